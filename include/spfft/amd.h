@@ -1,0 +1,102 @@
+/*
+ * SpFFT-AMD C extensions (not part of the SpFFT reference API):
+ *  - communicators that do not need MPI (callbacks, in-process local group),
+ *  - distributed grids over such communicators,
+ *  - explicit HIP streams / asynchronous execution, step-wise execution,
+ *  - timing report (host timer tree, JSON) and last-error text.
+ */
+#ifndef SPFFT_AMD_H
+#define SPFFT_AMD_H
+
+#include <stddef.h>
+
+#include "spfft/config.h"
+#include "spfft/errors.h"
+#include "spfft/grid.h"
+#include "spfft/grid_float.h"
+#include "spfft/transform.h"
+#include "spfft/transform_float.h"
+#include "spfft/types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* SpfftAmdComm;
+
+/* A communicator implemented by the caller. Each function returns 0 on success.
+ *  allgather: every rank contributes `bytes`; recv holds size*bytes in rank order.
+ *  alltoallv: host buffers, counts and displacements in bytes (size entries each).
+ *  destroy:   optional, called once when the last user of the communicator is gone. */
+typedef struct SpfftAmdCommCallbacks {
+  void* context;
+  int rank;
+  int size;
+  int (*allgather)(void* context, const void* send, void* recv, size_t bytes);
+  int (*alltoallv)(void* context, const void* send, const size_t* sendCounts,
+                   const size_t* sendDispls, void* recv, const size_t* recvCounts,
+                   const size_t* recvDispls);
+  int (*barrier)(void* context);
+  void (*destroy)(void* context);
+} SpfftAmdCommCallbacks;
+
+SPFFT_EXPORT SpfftError spfft_amd_comm_create_callbacks(SpfftAmdComm* comm,
+                                                        const SpfftAmdCommCallbacks* callbacks);
+/* Creates `size` communicators of one in-process group (comms[r] has rank r). */
+SPFFT_EXPORT SpfftError spfft_amd_comm_create_local_group(int size, SpfftAmdComm* comms);
+SPFFT_EXPORT SpfftError spfft_amd_comm_destroy(SpfftAmdComm comm);
+SPFFT_EXPORT SpfftError spfft_amd_comm_rank(SpfftAmdComm comm, int* rank);
+SPFFT_EXPORT SpfftError spfft_amd_comm_size(SpfftAmdComm comm, int* size);
+
+SPFFT_EXPORT SpfftError spfft_amd_grid_create_distributed(
+    SpfftGrid* grid, int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+    int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads,
+    SpfftAmdComm comm, SpfftExchangeType exchangeType);
+SPFFT_EXPORT SpfftError spfft_amd_float_grid_create_distributed(
+    SpfftFloatGrid* grid, int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+    int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads,
+    SpfftAmdComm comm, SpfftExchangeType exchangeType);
+SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchangeType* type);
+SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
+                                                           SpfftExchangeType* type);
+
+/* Execute on `hipStream` (hipStream_t). synchronous = 0: return after enqueue. */
+SPFFT_EXPORT SpfftError spfft_amd_transform_set_stream(SpfftTransform transform, void* hipStream,
+                                                       int synchronous);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_set_stream(SpfftFloatTransform transform,
+                                                             void* hipStream, int synchronous);
+SPFFT_EXPORT SpfftError spfft_amd_transform_synchronize(SpfftTransform transform);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_synchronize(SpfftFloatTransform transform);
+SPFFT_EXPORT SpfftError spfft_amd_transform_local_z_offset_rank(SpfftTransform transform, int rank,
+                                                                int* offset, int* length);
+
+/* Step-wise execution (forward: xy, exchange, z; backward: z, exchange, xy). */
+SPFFT_EXPORT SpfftError spfft_amd_transform_forward_xy(SpfftTransform t,
+                                                       SpfftProcessingUnitType inputLocation);
+SPFFT_EXPORT SpfftError spfft_amd_transform_forward_exchange(SpfftTransform t, int nonBlocking);
+SPFFT_EXPORT SpfftError spfft_amd_transform_forward_z(SpfftTransform t, double* output,
+                                                      SpfftScalingType scaling);
+SPFFT_EXPORT SpfftError spfft_amd_transform_backward_z(SpfftTransform t, const double* input);
+SPFFT_EXPORT SpfftError spfft_amd_transform_backward_exchange(SpfftTransform t, int nonBlocking);
+SPFFT_EXPORT SpfftError spfft_amd_transform_backward_xy(SpfftTransform t,
+                                                        SpfftProcessingUnitType outputLocation);
+
+/* Host timer tree (enabled by SPFFT_TIMING=1 or spfft_amd_timing_enable(1)). */
+SPFFT_EXPORT SpfftError spfft_amd_timing_enable(int enable);
+SPFFT_EXPORT SpfftError spfft_amd_timing_reset(void);
+/* Writes a JSON report into buffer (truncated to size-1); *required = full length + 1. */
+SPFFT_EXPORT SpfftError spfft_amd_timing_json(char* buffer, size_t size, size_t* required);
+SPFFT_EXPORT SpfftError spfft_amd_timing_print(char* buffer, size_t size, size_t* required);
+
+/* Text of the last error raised in this thread (empty if none). */
+SPFFT_EXPORT const char* spfft_amd_last_error_message(void);
+/* Number of HIP devices visible (0 when no GPU runtime/device). */
+SPFFT_EXPORT int spfft_amd_device_count(void);
+/* Library build information ("gfx950", version, ...). */
+SPFFT_EXPORT const char* spfft_amd_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,54 @@
+/*
+ * spfft::Communicator — the control-plane / host-data-plane abstraction of
+ * SpFFT-AMD (SpFFT-AMD addition; the reference hard-wires MPI, see
+ * src/mpi_util/mpi_communicator_handle.hpp:43-74).
+ *
+ * Implementations shipped:
+ *  - MPI (libspfft_amd_mpi, wraps a duplicated MPI_Comm),
+ *  - callbacks (C API; used by the Python front end over torch.distributed),
+ *  - an in-process "local group" of N ranks driven by N threads (tests, and
+ *    P-virtual-rank runs on a single GPU).
+ * The GPU data plane (RCCL over xGMI) is bootstrapped through allgather().
+ */
+#ifndef SPFFT_COMMUNICATOR_HPP
+#define SPFFT_COMMUNICATOR_HPP
+
+#include <cstddef>
+#include <memory>
+#include <vector>
+
+#include "spfft/config.h"
+
+namespace spfft {
+
+class SPFFT_EXPORT Communicator {
+public:
+  virtual ~Communicator();
+
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+
+  /* Every rank contributes `bytes` bytes; recv receives size()*bytes in rank order. */
+  virtual void allgather(const void* send, void* recv, std::size_t bytes) = 0;
+
+  /* Host-memory all-to-all with per-peer byte counts and byte displacements. */
+  virtual void alltoallv(const void* send, const std::size_t* sendCounts,
+                         const std::size_t* sendDispls, void* recv, const std::size_t* recvCounts,
+                         const std::size_t* recvDispls) = 0;
+
+  virtual void barrier();
+
+  /* A communicator with the same members but an independent message space. */
+  virtual std::shared_ptr<Communicator> duplicate() const = 0;
+
+  /* True for the in-process local group (GPU data plane uses peer copies instead of RCCL). */
+  virtual bool is_local_group() const { return false; }
+};
+
+/* Creates `size` communicators forming one in-process group; element r has rank r.
+ * Each must be driven by its own thread (collectives block until all arrive). */
+SPFFT_EXPORT std::vector<std::shared_ptr<Communicator>> create_local_communicators(int size);
+
+}  // namespace spfft
+
+#endif

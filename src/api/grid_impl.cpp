@@ -1,0 +1,173 @@
+#include "api/grid_impl.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <thread>
+#include <vector>
+
+#include "gpu/device_comm.hpp"
+#include "gpu/gpu_runtime.hpp"
+#include "spfft/exceptions.hpp"
+
+namespace spfft {
+
+namespace {
+int resolve_threads(int n) {
+  if (n >= 1) return n;
+  const unsigned hw = std::thread::hardware_concurrency();
+  return hw ? static_cast<int>(hw) : 1;
+}
+bool valid_pu(SpfftProcessingUnitType pu) { return (pu & (SPFFT_PU_HOST | SPFFT_PU_GPU)) != 0; }
+}  // namespace
+
+template <typename T>
+void GridImpl<T>::init(int maxDimX, int maxDimY, int maxDimZ, int maxSticks, int maxLocalZ,
+                       SpfftProcessingUnitType pu, int numThreads) {
+  // argument checks (reference: grid_internal.cpp:60-66, 131-145)
+  if (maxDimX <= 0 || maxDimY <= 0 || maxDimZ <= 0 || maxSticks < 0 || maxLocalZ < 0)
+    throw InvalidParameterError();
+  if (!valid_pu(pu)) throw InvalidParameterError();
+  maxX_ = maxDimX;
+  maxY_ = maxDimY;
+  maxZ_ = maxDimZ;
+  maxSticks_ = maxSticks;
+  maxLocalZ_ = maxLocalZ;
+  pu_ = pu;
+  numThreads_ = resolve_threads(numThreads);
+  // 64-bit sizes; the public API keeps int (reference quirk: int views, gpu_array_view.hpp:71)
+  planeElems_ = checked_mul(checked_mul(maxX_, maxY_), std::max(1, maxLocalZ_));
+  exchElems_ = std::max(planeElems_, checked_mul(maxZ_, maxSticks_));
+  if (pu_ & SPFFT_PU_GPU) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+      (void)hipGetLastError();
+      throw GPUNoDeviceError();
+    }
+    deviceId_ = current_device();
+  }
+}
+
+template <typename T>
+GridImpl<T>::GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+                      SpfftProcessingUnitType pu, int numThreads) {
+  init(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxDimZ, pu, numThreads);
+  if (pu_ & SPFFT_PU_GPU) allocate_device();
+}
+
+template <typename T>
+GridImpl<T>::GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+                      int maxLocalZLength, SpfftProcessingUnitType pu, int numThreads,
+                      std::shared_ptr<Communicator> comm, SpfftExchangeType exchangeType) {
+  if (!comm) throw InvalidParameterError();
+  comm_ = comm->duplicate();
+  // local validation first, then a collective agreement on PU / exchange / errors
+  // (reference: grid_internal.cpp:147-167) so no rank is left inside a collective.
+  int status = 0;
+  if (maxDimX <= 0 || maxDimY <= 0 || maxDimZ <= 0 || maxNumLocalZColumns < 0 ||
+      maxLocalZLength < 0 || !valid_pu(pu))
+    status = 1;
+  if (exchangeType < SPFFT_EXCH_DEFAULT || exchangeType > SPFFT_EXCH_UNBUFFERED) status = 1;
+  struct Info {
+    int status, pu, exch, maxSticks, maxLocalZ;
+  };
+  Info mine{status, static_cast<int>(pu), static_cast<int>(exchangeType), maxNumLocalZColumns,
+            maxLocalZLength};
+  std::vector<Info> all(comm_->size());
+  comm_->allgather(&mine, all.data(), sizeof(Info));
+  int gMaxSticks = 0, gMaxLocalZ = 0;
+  for (const auto& i : all) {
+    if (i.status) {
+      if (status) throw InvalidParameterError();
+      throw MPIParameterMismatchError();
+    }
+    if (i.pu != mine.pu || i.exch != mine.exch) throw MPIParameterMismatchError();
+    gMaxSticks = std::max(gMaxSticks, i.maxSticks);
+    gMaxLocalZ = std::max(gMaxLocalZ, i.maxLocalZ);
+  }
+  exchange_ = exchangeType == SPFFT_EXCH_DEFAULT ? SPFFT_EXCH_COMPACT_BUFFERED : exchangeType;
+  init(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength, pu, numThreads);
+  if (comm_->size() > 1 && is_exchange_buffered(exchange_)) {
+    const i64 padded = checked_mul(checked_mul(gMaxSticks, gMaxLocalZ), comm_->size());
+    exchElems_ = std::max(exchElems_, padded);
+  }
+  if (pu_ & SPFFT_PU_GPU) allocate_device();
+}
+
+template <typename T>
+GridImpl<T>::GridImpl(const GridImpl& o)
+    : maxX_(o.maxX_),
+      maxY_(o.maxY_),
+      maxZ_(o.maxZ_),
+      maxSticks_(o.maxSticks_),
+      maxLocalZ_(o.maxLocalZ_),
+      pu_(o.pu_),
+      numThreads_(o.numThreads_),
+      deviceId_(o.deviceId_),
+      exchange_(o.exchange_),
+      comm_(o.comm_ ? o.comm_->duplicate() : nullptr),
+      exchElems_(o.exchElems_),
+      planeElems_(o.planeElems_) {
+  if (pu_ & SPFFT_PU_GPU) {
+    DeviceGuard guard(deviceId_);
+    allocate_device();
+  }
+}
+
+template <typename T>
+GridImpl<T>::~GridImpl() {
+  if (pu_ & SPFFT_PU_GPU) {
+    // release device resources on the grid's device
+    try {
+      DeviceGuard guard(deviceId_);
+      devComm_.reset();
+      for (auto& d : dev_) d.reset();
+    } catch (...) {
+    }
+  }
+}
+
+template <typename T>
+ThreadPool& GridImpl<T>::pool() {
+  std::lock_guard<std::mutex> lock(allocMutex_);
+  if (!pool_) pool_.reset(new ThreadPool(numThreads_));
+  return *pool_;
+}
+
+template <typename T>
+void GridImpl<T>::allocate_device() {
+  const std::size_t cb = sizeof(T) * 2;
+  dev_[kStickSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
+  if (!local()) dev_[kSlabSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
+  dev_[kInter].reset(new DeviceBuffer(static_cast<std::size_t>(planeElems_) * cb));
+  dev_[kSpace].reset(new DeviceBuffer(static_cast<std::size_t>(planeElems_) * cb));
+}
+
+template <typename T>
+void* GridImpl<T>::host_slot(Slot s) {
+  std::lock_guard<std::mutex> lock(allocMutex_);
+  if (s == kSlabSide && local()) s = kStickSide;
+  if (!host_[s].data()) {
+    const std::size_t elems = static_cast<std::size_t>(slot_elements(s));
+    host_[s].allocate(std::max<std::size_t>(1, elems) * sizeof(T) * 2, (pu_ & SPFFT_PU_GPU) != 0);
+  }
+  return host_[s].data();
+}
+
+template <typename T>
+void* GridImpl<T>::device_slot(Slot s) {
+  if (!(pu_ & SPFFT_PU_GPU)) throw InvalidParameterError();
+  if (s == kSlabSide && local()) s = kStickSide;
+  return dev_[s]->data();
+}
+
+template <typename T>
+DeviceComm& GridImpl<T>::device_comm() {
+  std::lock_guard<std::mutex> lock(allocMutex_);
+  if (!devComm_) devComm_ = DeviceComm::create(comm_, deviceId_);
+  return *devComm_;
+}
+
+template class GridImpl<double>;
+template class GridImpl<float>;
+
+}  // namespace spfft

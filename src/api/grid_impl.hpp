@@ -1,0 +1,84 @@
+// GridImpl<T>: the memory arena + communicator shared by all transforms of a
+// Grid (reference: src/spfft/grid_internal.{hpp,cpp}). Buffers are sized for the
+// grid maxima so any transform up to those sizes runs without allocation.
+#pragma once
+
+#include <memory>
+#include <mutex>
+
+#include "core/common.hpp"
+#include "core/host_buffer.hpp"
+#include "core/thread_pool.hpp"
+#include "spfft/communicator.hpp"
+#include "spfft/types.h"
+
+namespace spfft {
+
+class DeviceBuffer;   // gpu/device_buffer.hpp
+class DeviceComm;     // gpu/device_comm.hpp
+
+template <typename T>
+class GridImpl {
+public:
+  // Local grid.
+  GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+           SpfftProcessingUnitType pu, int numThreads);
+  // Distributed grid (collective over comm).
+  GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns, int maxLocalZLength,
+           SpfftProcessingUnitType pu, int numThreads, std::shared_ptr<Communicator> comm,
+           SpfftExchangeType exchangeType);
+  // Deep copy: new buffers, duplicated communicator (collective if distributed).
+  GridImpl(const GridImpl& other);
+  ~GridImpl();
+
+  int max_dim_x() const { return maxX_; }
+  int max_dim_y() const { return maxY_; }
+  int max_dim_z() const { return maxZ_; }
+  int max_num_local_z_columns() const { return maxSticks_; }
+  int max_local_z_length() const { return maxLocalZ_; }
+  SpfftProcessingUnitType processing_unit() const { return pu_; }
+  int device_id() const { return deviceId_; }
+  int num_threads() const { return numThreads_; }
+  SpfftExchangeType exchange_type() const { return exchange_; }
+  bool local() const { return !comm_ || comm_->size() == 1; }
+  const std::shared_ptr<Communicator>& communicator() const { return comm_; }
+
+  ThreadPool& pool();
+
+  // Buffer slots (complex<T> element counts fixed at construction).
+  enum Slot { kStickSide = 0, kSlabSide = 1, kInter = 2, kSpace = 3, kNumSlots = 4 };
+  i64 slot_elements(Slot s) const { return s == kStickSide || s == kSlabSide ? exchElems_ : planeElems_; }
+
+  // Host memory (allocated on first use; pinned if the grid has the GPU bit).
+  void* host_slot(Slot s);
+  // Device memory (GPU grids only).
+  void* device_slot(Slot s);
+
+  // RCCL / peer-copy data plane (GPU distributed grids), created on first use.
+  DeviceComm& device_comm();
+
+  // Transforms of one grid share buffers; execution is serialised by this lock.
+  std::mutex& exec_mutex() { return execMutex_; }
+
+private:
+  void init(int maxDimX, int maxDimY, int maxDimZ, int maxSticks, int maxLocalZ,
+            SpfftProcessingUnitType pu, int numThreads);
+  void allocate_device();
+
+  int maxX_ = 0, maxY_ = 0, maxZ_ = 0, maxSticks_ = 0, maxLocalZ_ = 0;
+  SpfftProcessingUnitType pu_ = SPFFT_PU_HOST;
+  int numThreads_ = 1;
+  int deviceId_ = 0;
+  SpfftExchangeType exchange_ = SPFFT_EXCH_COMPACT_BUFFERED;
+  std::shared_ptr<Communicator> comm_;
+  i64 exchElems_ = 0, planeElems_ = 0;
+
+  std::unique_ptr<ThreadPool> pool_;
+  HostBuffer host_[kNumSlots];
+  std::unique_ptr<DeviceBuffer> dev_[kNumSlots];
+  std::unique_ptr<DeviceComm> devComm_;
+  std::mutex allocMutex_;
+  std::mutex execMutex_;
+};
+
+}  // namespace spfft

@@ -1,0 +1,136 @@
+// Overlapped execution of independent transforms
+// (reference: src/spfft/multi_transform_internal.hpp:47-145).
+//
+// GPU transforms each own a stream, so enqueuing stage k of every transform
+// before stage k+1 lets the GPU overlap transform i's exchange with transform
+// j's FFT kernels; host transforms run their stages in between.
+#include <set>
+#include <vector>
+
+#include "api/transform_impl.hpp"
+#include "core/timing.hpp"
+#include "spfft/multi_transform.hpp"
+#include "spfft/multi_transform_float.hpp"
+
+namespace spfft {
+namespace {
+
+template <typename T>
+void check_distinct_grids(const std::vector<TransformImpl<T>*>& ts) {
+  std::set<const GridImpl<T>*> grids;
+  for (auto* t : ts) {
+    if (!t) throw InvalidParameterError();
+    if (!grids.insert(t->grid().get()).second) throw InvalidParameterError();
+  }
+}
+
+template <typename T>
+void multi_forward(const std::vector<TransformImpl<T>*>& ts,
+                   const SpfftProcessingUnitType* inputLocations, T* const* outputs,
+                   const SpfftScalingType* scalings) {
+  SPFFT_TIMED_SCOPE("multi_forward");
+  check_distinct_grids(ts);
+  const int n = static_cast<int>(ts.size());
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu()) ts[i]->forward_xy(inputLocations[i]);
+  for (int i = 0; i < n; ++i)
+    if (!ts[i]->is_gpu()) {
+      ts[i]->forward_xy(inputLocations[i]);
+      ts[i]->forward_exchange(true);
+    }
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu()) {
+      ts[i]->forward_exchange(true);
+      ts[i]->forward_z(outputs[i], scalings[i]);
+    }
+  for (int i = 0; i < n; ++i)
+    if (!ts[i]->is_gpu()) ts[i]->forward_z(outputs[i], scalings[i]);
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu() && ts[i]->gpu()->synchronous()) ts[i]->synchronize();
+}
+
+template <typename T>
+void multi_backward(const std::vector<TransformImpl<T>*>& ts, const T* const* inputs,
+                    const SpfftProcessingUnitType* outputLocations) {
+  SPFFT_TIMED_SCOPE("multi_backward");
+  check_distinct_grids(ts);
+  const int n = static_cast<int>(ts.size());
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu()) ts[i]->backward_z(inputs[i]);
+  for (int i = 0; i < n; ++i)
+    if (!ts[i]->is_gpu()) {
+      ts[i]->backward_z(inputs[i]);
+      ts[i]->backward_exchange(true);
+    }
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu()) {
+      ts[i]->backward_exchange(true);
+      ts[i]->backward_xy(outputLocations[i]);
+    }
+  for (int i = 0; i < n; ++i)
+    if (!ts[i]->is_gpu()) ts[i]->backward_xy(outputLocations[i]);
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu() && ts[i]->gpu()->synchronous()) ts[i]->synchronize();
+}
+
+template <typename TR, typename T>
+std::vector<TransformImpl<T>*> impls(int n, TR* transforms) {
+  if (n < 0 || (n > 0 && !transforms)) throw InvalidParameterError();
+  std::vector<TransformImpl<T>*> v;
+  for (int i = 0; i < n; ++i) v.push_back(transforms[i].impl().get());
+  return v;
+}
+
+}  // namespace
+
+void multi_transform_forward(int numTransforms, Transform* transforms,
+                             SpfftProcessingUnitType* inputLocations, double** outputPointers,
+                             SpfftScalingType* scalingTypes) {
+  multi_forward<double>(impls<Transform, double>(numTransforms, transforms), inputLocations,
+                        outputPointers, scalingTypes);
+}
+
+void multi_transform_backward(int numTransforms, Transform* transforms, double** inputPointers,
+                              SpfftProcessingUnitType* outputLocations) {
+  multi_backward<double>(impls<Transform, double>(numTransforms, transforms), inputPointers,
+                         outputLocations);
+}
+
+void multi_transform_forward(int numTransforms, TransformFloat* transforms,
+                             SpfftProcessingUnitType* inputLocations, float** outputPointers,
+                             SpfftScalingType* scalingTypes) {
+  multi_forward<float>(impls<TransformFloat, float>(numTransforms, transforms), inputLocations,
+                       outputPointers, scalingTypes);
+}
+
+void multi_transform_backward(int numTransforms, TransformFloat* transforms, float** inputPointers,
+                              SpfftProcessingUnitType* outputLocations) {
+  multi_backward<float>(impls<TransformFloat, float>(numTransforms, transforms), inputPointers,
+                        outputLocations);
+}
+
+// used by the C API (array of handles)
+void multi_forward_handles(int n, Transform** ts, SpfftProcessingUnitType* in, double** out,
+                           SpfftScalingType* sc) {
+  std::vector<TransformImpl<double>*> v;
+  for (int i = 0; i < n; ++i) v.push_back(ts[i] ? ts[i]->impl().get() : nullptr);
+  multi_forward<double>(v, in, out, sc);
+}
+void multi_backward_handles(int n, Transform** ts, double** in, SpfftProcessingUnitType* out) {
+  std::vector<TransformImpl<double>*> v;
+  for (int i = 0; i < n; ++i) v.push_back(ts[i] ? ts[i]->impl().get() : nullptr);
+  multi_backward<double>(v, in, out);
+}
+void multi_forward_handles(int n, TransformFloat** ts, SpfftProcessingUnitType* in, float** out,
+                           SpfftScalingType* sc) {
+  std::vector<TransformImpl<float>*> v;
+  for (int i = 0; i < n; ++i) v.push_back(ts[i] ? ts[i]->impl().get() : nullptr);
+  multi_forward<float>(v, in, out, sc);
+}
+void multi_backward_handles(int n, TransformFloat** ts, float** in, SpfftProcessingUnitType* out) {
+  std::vector<TransformImpl<float>*> v;
+  for (int i = 0; i < n; ++i) v.push_back(ts[i] ? ts[i]->impl().get() : nullptr);
+  multi_backward<float>(v, in, out);
+}
+
+}  // namespace spfft

@@ -1,0 +1,40 @@
+// Host timing tree + roctx ranges (replaces the reference's rt_graph timer,
+// src/timing/rt_graph.hpp:107-173, timing.hpp:45-60).
+//
+// Scopes form a tree per call path; each node keeps every sample so the report
+// has count / total / mean / median / min / max / share of parent. Enabled at
+// run time (SPFFT_TIMING=1 or spfft_amd_timing_enable). Independently of that,
+// every scope emits a roctx range (visible with rocprofv3 --marker-trace).
+#pragma once
+
+#include <string>
+
+namespace spfft {
+namespace timing {
+
+bool enabled();
+void set_enabled(bool on);
+void reset();
+std::string report_json();
+std::string report_text();
+
+class Scope {
+public:
+  explicit Scope(const char* name);
+  ~Scope();
+  Scope(const Scope&) = delete;
+  Scope& operator=(const Scope&) = delete;
+
+private:
+  void* node_ = nullptr;
+  long long startNs_ = 0;
+  bool marker_ = false;
+};
+
+}  // namespace timing
+}  // namespace spfft
+
+#define SPFFT_TIMING_CONCAT2(a, b) a##b
+#define SPFFT_TIMING_CONCAT(a, b) SPFFT_TIMING_CONCAT2(a, b)
+#define SPFFT_TIMED_SCOPE(name) \
+  ::spfft::timing::Scope SPFFT_TIMING_CONCAT(spfftTimingScope_, __LINE__)(name)

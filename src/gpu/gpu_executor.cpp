@@ -1,0 +1,312 @@
+#include "gpu/gpu_executor.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "core/timing.hpp"
+#include "fft/fft_plan.hpp"
+#include "gpu/device_comm.hpp"
+#include "spfft/exceptions.hpp"
+
+namespace spfft {
+
+template <typename T>
+template <typename U>
+U* GpuExecutor<T>::upload(std::unique_ptr<DeviceBuffer>& buf, const std::vector<U>& v) {
+  if (v.empty()) return nullptr;
+  buf.reset(new DeviceBuffer(v.size() * sizeof(U)));
+  gpu_check(hipMemcpy(buf->data(), v.data(), v.size() * sizeof(U), hipMemcpyHostToDevice),
+            "hipMemcpy");
+  return buf->data<U>();
+}
+
+template <typename T>
+GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
+                            std::shared_ptr<const IndexPlan> plan)
+    : grid_(std::move(grid)), plan_(std::move(plan)), deviceId_(grid_->device_id()) {
+  DeviceGuard guard(deviceId_);
+  const IndexPlan& p = *plan_;
+  const bool distributed = p.size > 1;
+  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()));
+  floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
+  if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
+      layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
+    throw InvalidParameterError();
+  for (int n : {p.dimX, p.dimY, p.dimZ}) {
+    if (!dev::has_ct_kernel(n) && n > dev::max_device_fft_length(sizeof(T) == 8))
+      throw GPUFFTError();
+  }
+
+  ownStream_.reset(new GpuStream());
+  stream_ = ownStream_->get();
+  event_.reset(new GpuEvent());
+
+  // device tables (uploaded once; the hot path never touches the host plan)
+  upload(runs_, p.runs);
+  upload(runOffsets_, p.stickRunOffsets);
+  std::vector<int> zRank(p.dimZ, 0);
+  for (int r = 0; r < p.size; ++r)
+    for (int z = 0; z < p.planesPerRank[r]; ++z) zRank[p.planeOffsets[r] + z] = r;
+  upload(zRank_, zRank);
+  std::vector<long long> sd(layout_.stickDispl.begin(), layout_.stickDispl.end());
+  std::vector<long long> ss(layout_.stickStride.begin(), layout_.stickStride.end());
+  upload(segDispl_, sd);
+  upload(segStride_, ss);
+  upload(segZOff_, p.planeOffsets);
+  upload(colOffsets_, p.colOffsets);
+  upload(colY_, p.colY);
+  std::vector<long long> cb(layout_.colEntryBase.begin(), layout_.colEntryBase.end());
+  upload(colBase_, cb);
+  upload(colX_, p.colX);
+  upload(twX_, make_twiddles<T>(p.dimX));
+  upload(twY_, make_twiddles<T>(p.dimY));
+  upload(twZ_, make_twiddles<T>(p.dimZ));
+
+  if (distributed) {
+    const std::int64_t eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+    for (int r = 0; r < p.size; ++r) {
+      bwdSendCounts_.push_back(layout_.stickCount[r] * eb);
+      bwdSendDispls_.push_back(layout_.stickDispl[r] * eb);
+      bwdRecvCounts_.push_back(layout_.slabCount[r] * eb);
+      bwdRecvDispls_.push_back(layout_.slabDispl[r] * eb);
+    }
+    grid_->device_comm();  // collective data-plane setup happens at plan time
+  }
+}
+
+template <typename T>
+GpuExecutor<T>::~GpuExecutor() {
+  try {
+    DeviceGuard guard(deviceId_);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+  } catch (...) {
+  }
+}
+
+template <typename T>
+void GpuExecutor<T>::set_stream(hipStream_t stream, bool synchronous) {
+  stream_ = stream ? stream : ownStream_->get();
+  synchronous_ = synchronous;
+}
+
+template <typename T>
+void GpuExecutor<T>::synchronize() {
+  DeviceGuard guard(deviceId_);
+  gpu_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+template <typename T>
+void GpuExecutor<T>::order_after_default_stream() {
+  // errors left behind by earlier (user) GPU work (reference: execution_gpu.cpp:251-253)
+  if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
+  if (stream_ == ownStream_->get()) {
+    // order after work already queued on the legacy default stream (reference: execution_gpu.cpp:258-259)
+    event_->record(nullptr);
+    event_->wait_on(stream_);
+  }
+}
+
+template <typename T>
+cx<T>* GpuExecutor<T>::staging(std::size_t elems) {
+  const std::size_t bytes = std::max<std::size_t>(1, elems) * sizeof(cx<T>);
+  if (!staging_ || staging_->bytes() < bytes) staging_.reset(new DeviceBuffer(bytes));
+  return staging_->data<cx<T>>();
+}
+
+template <typename T>
+std::size_t GpuExecutor<T>::space_bytes() const {
+  const IndexPlan& p = *plan_;
+  const std::size_t elems = static_cast<std::size_t>(p.local_planes()) * p.dimY * p.dimX;
+  return elems * (p.type == SPFFT_TRANS_R2C ? sizeof(T) : sizeof(cx<T>));
+}
+
+template <typename T>
+T* GpuExecutor<T>::space_domain(SpfftProcessingUnitType location) {
+  if (location == SPFFT_PU_GPU) return static_cast<T*>(grid_->device_slot(GridImpl<T>::kSpace));
+  if (location == SPFFT_PU_HOST) return static_cast<T*>(grid_->host_slot(GridImpl<T>::kSpace));
+  throw InvalidParameterError();
+}
+
+template <typename T>
+dev::ZArgs GpuExecutor<T>::zargs() const {
+  const IndexPlan& p = *plan_;
+  dev::ZArgs a{};
+  a.numSticks = p.local_sticks();
+  a.n = p.dimZ;
+  a.zeroStick = p.type == SPFFT_TRANS_R2C ? p.zeroStick : -1;
+  a.runs = runs_ ? runs_->data<StickRun>() : nullptr;
+  a.runOffsets = runOffsets_ ? runOffsets_->data<int>() : nullptr;
+  a.single = p.size == 1 ? 1 : 0;
+  a.zRank = zRank_ ? zRank_->data<int>() : nullptr;
+  a.segDispl = segDispl_ ? segDispl_->data<long long>() : nullptr;
+  a.segStride = segStride_ ? segStride_->data<long long>() : nullptr;
+  a.segZOff = segZOff_ ? segZOff_->data<int>() : nullptr;
+  return a;
+}
+
+template <typename T>
+dev::YArgs GpuExecutor<T>::yargs() const {
+  const IndexPlan& p = *plan_;
+  dev::YArgs a{};
+  a.ncols = p.num_columns();
+  a.L = p.local_planes();
+  a.n = p.dimY;
+  a.colOfX0 = p.type == SPFFT_TRANS_R2C ? p.colOfX0 : -1;
+  a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
+  a.colY = colY_ ? colY_->data<int>() : nullptr;
+  a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
+  return a;
+}
+
+template <typename T>
+dev::XArgs GpuExecutor<T>::xargs() const {
+  const IndexPlan& p = *plan_;
+  dev::XArgs a{};
+  a.L = p.local_planes();
+  a.Y = p.dimY;
+  a.n = p.dimX;
+  a.nFreq = p.dimXFreq;
+  a.ncols = p.num_columns();
+  a.colX = colX_ ? colX_->data<int>() : nullptr;
+  return a;
+}
+
+// ------------------------------------------------------------------ backward
+template <typename T>
+void GpuExecutor<T>::backward_z(const T* input) {
+  SPFFT_TIMED_SCOPE("gpu_backward_z");
+  DeviceGuard guard(deviceId_);
+  order_after_default_stream();
+  const IndexPlan& p = *plan_;
+  const cx<T>* values = reinterpret_cast<const cx<T>*>(input);
+  if (p.numLocalElements > 0) {
+    if (!input) throw InvalidParameterError();
+    if (!is_device_pointer(input)) {
+      cx<T>* st = staging(p.numLocalElements);
+      gpu_check(hipMemcpyAsync(st, input, sizeof(cx<T>) * p.numLocalElements,
+                               hipMemcpyHostToDevice, stream_),
+                "hipMemcpyAsync");
+      values = st;
+    }
+  }
+  void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  const auto a = zargs();
+  if (floatExchange_)
+    dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
+                                         twZ_->data<cx<T>>(), stream_);
+  else
+    dev::launch_z_backward<T, cx<T>>(a, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
+                                     stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::exchange(bool backward) {
+  if (plan_->size <= 1) return;
+  DeviceGuard guard(deviceId_);
+  void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
+  DeviceComm& dc = grid_->device_comm();
+  if (backward)
+    dc.alltoallv(stick, bwdSendCounts_.data(), bwdSendDispls_.data(), slab, bwdRecvCounts_.data(),
+                 bwdRecvDispls_.data(), stream_);
+  else
+    dc.alltoallv(slab, bwdRecvCounts_.data(), bwdRecvDispls_.data(), stick, bwdSendCounts_.data(),
+                 bwdSendDispls_.data(), stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
+  SPFFT_TIMED_SCOPE("gpu_backward_exchange");
+  exchange(true);
+}
+
+template <typename T>
+void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
+  SPFFT_TIMED_SCOPE("gpu_backward_xy");
+  if (outputLocation != SPFFT_PU_HOST && outputLocation != SPFFT_PU_GPU)
+    throw InvalidParameterError();
+  DeviceGuard guard(deviceId_);
+  void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
+  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  void* space = grid_->device_slot(GridImpl<T>::kSpace);
+  const auto ya = yargs();
+  if (floatExchange_)
+    dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
+                                         twY_->data<cx<T>>(), stream_);
+  else
+    dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
+                                     twY_->data<cx<T>>(), stream_);
+  dev::launch_x_backward<T>(xargs(), plan_->type == SPFFT_TRANS_R2C, inter, space,
+                            twX_->data<cx<T>>(), stream_);
+  if (outputLocation == SPFFT_PU_HOST) {
+    gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
+                             hipMemcpyDeviceToHost, stream_),
+              "hipMemcpyAsync");
+  }
+}
+
+// ------------------------------------------------------------------- forward
+template <typename T>
+void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
+  SPFFT_TIMED_SCOPE("gpu_forward_xy");
+  if (inputLocation != SPFFT_PU_HOST && inputLocation != SPFFT_PU_GPU)
+    throw InvalidParameterError();
+  DeviceGuard guard(deviceId_);
+  order_after_default_stream();
+  void* space = grid_->device_slot(GridImpl<T>::kSpace);
+  if (inputLocation == SPFFT_PU_HOST) {
+    gpu_check(hipMemcpyAsync(space, grid_->host_slot(GridImpl<T>::kSpace), space_bytes(),
+                             hipMemcpyHostToDevice, stream_),
+              "hipMemcpyAsync");
+  }
+  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
+  dev::launch_x_forward<T>(xargs(), plan_->type == SPFFT_TRANS_R2C, space, inter,
+                           twX_->data<cx<T>>(), stream_);
+  const auto ya = yargs();
+  if (floatExchange_)
+    dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+                                        twY_->data<cx<T>>(), stream_);
+  else
+    dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
+                                    stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
+  SPFFT_TIMED_SCOPE("gpu_forward_exchange");
+  exchange(false);
+}
+
+template <typename T>
+void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
+  SPFFT_TIMED_SCOPE("gpu_forward_z");
+  DeviceGuard guard(deviceId_);
+  const IndexPlan& p = *plan_;
+  const T factor =
+      scaling == SPFFT_FULL_SCALING
+          ? static_cast<T>(1.0 / (static_cast<double>(p.dimX) * p.dimY * p.dimZ))
+          : T(1);
+  cx<T>* values = reinterpret_cast<cx<T>*>(output);
+  const bool hostOut = p.numLocalElements > 0 && !is_device_pointer(output);
+  if (p.numLocalElements > 0 && !output) throw InvalidParameterError();
+  if (hostOut) values = staging(p.numLocalElements);
+  const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  const auto a = zargs();
+  if (floatExchange_)
+    dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,
+                                        twZ_->data<cx<T>>(), stream_);
+  else
+    dev::launch_z_forward<T, cx<T>>(a, static_cast<const cx<T>*>(stick), values, factor,
+                                    twZ_->data<cx<T>>(), stream_);
+  if (hostOut) {
+    gpu_check(hipMemcpyAsync(output, values, sizeof(cx<T>) * p.numLocalElements,
+                             hipMemcpyDeviceToHost, stream_),
+              "hipMemcpyAsync");
+  }
+}
+
+template class GpuExecutor<double>;
+template class GpuExecutor<float>;
+
+}  // namespace spfft

@@ -1,0 +1,68 @@
+// GPU execution engine (reference: src/execution/execution_gpu.{hpp,cpp}).
+//
+// Per direction three fused kernels (z, y, x stage) plus, for distributed
+// grids, one RCCL all-to-all(v) — all enqueued on one HIP stream without host
+// synchronisation; the call blocks only at the end (synchronous mode, the
+// SpFFT contract) or never (asynchronous mode with a user stream).
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "api/grid_impl.hpp"
+#include "gpu/gpu_runtime.hpp"
+#include "kernels/stage_args.hpp"
+#include "plan/index_plan.hpp"
+
+namespace spfft {
+
+template <typename T>
+class GpuExecutor {
+public:
+  GpuExecutor(std::shared_ptr<GridImpl<T>> grid, std::shared_ptr<const IndexPlan> plan);
+  ~GpuExecutor();
+
+  void backward_z(const T* input);
+  void backward_exchange(bool nonBlocking);
+  void backward_xy(SpfftProcessingUnitType outputLocation);
+  void forward_xy(SpfftProcessingUnitType inputLocation);
+  void forward_exchange(bool nonBlocking);
+  void forward_z(T* output, SpfftScalingType scaling);
+
+  void synchronize();
+  bool synchronous() const { return synchronous_; }
+  void set_stream(hipStream_t stream, bool synchronous);
+  hipStream_t stream() const { return stream_; }
+  T* space_domain(SpfftProcessingUnitType location);
+
+private:
+  template <typename U>
+  U* upload(std::unique_ptr<DeviceBuffer>& buf, const std::vector<U>& v);
+  void order_after_default_stream();
+  void exchange(bool backward);
+  dev::ZArgs zargs() const;
+  dev::YArgs yargs() const;
+  dev::XArgs xargs() const;
+  cx<T>* staging(std::size_t elems);
+  std::size_t space_bytes() const;
+
+  std::shared_ptr<GridImpl<T>> grid_;
+  std::shared_ptr<const IndexPlan> plan_;
+  ExchangeLayout layout_;
+  bool floatExchange_ = false;
+  int deviceId_ = 0;
+
+  std::unique_ptr<GpuStream> ownStream_;
+  hipStream_t stream_ = nullptr;
+  bool synchronous_ = true;
+  std::unique_ptr<GpuEvent> event_;
+
+  // device tables
+  std::unique_ptr<DeviceBuffer> runs_, runOffsets_, zRank_, segDispl_, segStride_, segZOff_;
+  std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
+  std::unique_ptr<DeviceBuffer> twX_, twY_, twZ_;
+  std::unique_ptr<DeviceBuffer> staging_;
+  std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;
+};
+
+}  // namespace spfft

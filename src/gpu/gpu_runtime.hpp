@@ -1,0 +1,86 @@
+// Thin HIP runtime layer (one backend: HIP on gfx950; no CUDA macros).
+// Error -> exception mapping as in the reference (src/gpu_util/gpu_runtime_api.hpp:112-124),
+// RAII stream/event/device-guard, pointer classification
+// (reference: src/gpu_util/gpu_pointer_translation.hpp:38-61).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+
+#include "spfft/exceptions.hpp"
+
+namespace spfft {
+
+[[noreturn]] void throw_gpu_error(hipError_t err, const char* what);
+
+inline void gpu_check(hipError_t err, const char* what = "") {
+  if (err != hipSuccess) throw_gpu_error(err, what);
+}
+
+// Debug mode (SPFFT_GPU_SYNC_DEBUG=1): synchronise and check after every launch
+// (reference: src/gpu_util/gpu_runtime.hpp:58-72 does this in Debug builds).
+bool gpu_sync_debug();
+void gpu_check_launch(const char* kernel, hipStream_t stream);
+
+class DeviceGuard {
+public:
+  explicit DeviceGuard(int device);
+  ~DeviceGuard();
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+private:
+  int previous_ = -1;
+  bool switched_ = false;
+};
+
+class GpuStream {
+public:
+  GpuStream();  // non-blocking stream on the current device
+  ~GpuStream();
+  GpuStream(const GpuStream&) = delete;
+  GpuStream& operator=(const GpuStream&) = delete;
+  hipStream_t get() const { return stream_; }
+
+private:
+  hipStream_t stream_ = nullptr;
+};
+
+class GpuEvent {
+public:
+  GpuEvent();  // timing disabled
+  ~GpuEvent();
+  GpuEvent(const GpuEvent&) = delete;
+  GpuEvent& operator=(const GpuEvent&) = delete;
+  hipEvent_t get() const { return event_; }
+  void record(hipStream_t s) { gpu_check(hipEventRecord(event_, s), "hipEventRecord"); }
+  void wait_on(hipStream_t s) { gpu_check(hipStreamWaitEvent(s, event_, 0), "hipStreamWaitEvent"); }
+
+private:
+  hipEvent_t event_ = nullptr;
+};
+
+class DeviceBuffer {
+public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(std::size_t bytes);
+  ~DeviceBuffer();
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  template <typename U = void>
+  U* data() const {
+    return static_cast<U*>(ptr_);
+  }
+  std::size_t bytes() const { return bytes_; }
+
+private:
+  void* ptr_ = nullptr;
+  std::size_t bytes_ = 0;
+};
+
+// true if ptr is device (or managed) memory accessible by the GPU kernels.
+bool is_device_pointer(const void* ptr);
+int current_device();
+
+}  // namespace spfft

@@ -1,0 +1,305 @@
+// Block-level FFT engines for CDNA4 (gfx950): a workgroup transforms B lines
+// of length N that sit in (or stream through) LDS.
+//
+//  FftCT<T, N, S>: compile-time length. Each lane keeps E = N/TP elements in
+//    VGPRs, executes E/R radix-R butterflies per Stockham pass and exchanges
+//    through LDS between passes (2 barriers per pass). LDS rows are padded by
+//    one element per 256-byte bank row, and consecutive lines start 16 bytes
+//    apart in the bank space, so both the strided pass writes and the
+//    column-wise gathers of the stage kernels are bank-conflict free.
+//  FftRT<T, S>: run-time length (any N, mixed radix incl. generic primes),
+//    ping-pong Stockham entirely in LDS. Used for lengths without a CT shape.
+//
+// Sign S = +1 is the backward (frequency -> space) direction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "fft/codelets.hpp"
+
+namespace spfft {
+namespace dev {
+
+constexpr int kMaxThreads = 256;
+constexpr int kLdsBudget = 64 * 1024;
+
+template <typename T>
+struct LdsGeom;
+template <>
+struct LdsGeom<double> {
+  static constexpr int kShift = 4;  // 16 x 16 B elements per 256 B bank row
+  static constexpr int kMod = 16;
+};
+template <>
+struct LdsGeom<float> {
+  static constexpr int kShift = 5;  // 32 x 8 B elements per bank row
+  static constexpr int kMod = 32;
+};
+
+template <typename T>
+__host__ __device__ constexpr int pad_index(int i) {
+  return i + (i >> LdsGeom<T>::kShift);
+}
+// Line stride: holds pad_index(N-1) and is == 1 (mod kMod) so that line b+1
+// starts one element further in the bank space than line b.
+template <typename T>
+__host__ __device__ constexpr int padded_stride(int n) {
+  return ((n + (n >> LdsGeom<T>::kShift) + LdsGeom<T>::kMod - 1) / LdsGeom<T>::kMod) *
+             LdsGeom<T>::kMod +
+         1;
+}
+
+// Lines per workgroup: as many as fit the LDS budget and the thread cap, with
+// the workgroup a whole number of waves.
+__host__ __device__ constexpr int lines_per_block(int tp, int lineBytes) {
+  int b = kMaxThreads / tp;
+  if (b * lineBytes > kLdsBudget) b = kLdsBudget / lineBytes;
+  if (b < 1) b = 1;
+  if (tp < 64) {
+    const int q = 64 / tp;
+    b = (b / q) * q;
+    if (b < q) b = q;
+  }
+  return b;
+}
+
+// --------------------------------------------------------------- CT shapes
+// E = elements per lane, R0..R2 = radices (1 = pass absent); every radix divides E.
+template <int N>
+struct CtShape;
+template <>
+struct CtShape<16> {
+  static constexpr int E = 16, R0 = 16, R1 = 1, R2 = 1;
+};
+template <>
+struct CtShape<32> {
+  static constexpr int E = 8, R0 = 8, R1 = 4, R2 = 1;
+};
+template <>
+struct CtShape<64> {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 1;
+};
+template <>
+struct CtShape<128> {
+  static constexpr int E = 16, R0 = 16, R1 = 8, R2 = 1;
+};
+template <>
+struct CtShape<256> {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 1;
+};
+template <>
+struct CtShape<512> {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8;
+};
+template <>
+struct CtShape<1024> {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 4;
+};
+
+struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
+
+template <typename T, int N, int S>
+struct FftCT {
+  using Sh = CtShape<N>;
+  static constexpr int E = Sh::E;
+  static constexpr int TP = N / E;  // lanes per line
+  static constexpr int LS = padded_stride<T>(N);
+  static constexpr int B = lines_per_block(TP, LS * static_cast<int>(sizeof(cx<T>)));
+  static constexpr int NT = B * TP;
+  static constexpr int RL = Sh::R2 > 1 ? Sh::R2 : (Sh::R1 > 1 ? Sh::R1 : Sh::R0);
+
+  static constexpr int lines() { return B; }
+  static constexpr int threads() { return NT; }
+  static constexpr std::size_t lds_bytes() { return std::size_t(B) * LS * sizeof(cx<T>); }
+  __device__ static int in_at(int b, int pos) { return b * LS + pad_index<T>(pos); }
+  __device__ static int out_at(int b, int pos) { return b * LS + pad_index<T>(pos); }
+
+  // butterflies of one pass on the lane's registers (input order: v[k*R + r]
+  // holds element j + r*N/R with j = t + k*TP)
+  template <int R, int NS>
+  __device__ static void compute(cx<T> (&v)[E], int t, const cx<T>* __restrict__ tw) {
+#pragma unroll
+    for (int k = 0; k < E / R; ++k) {
+      if (NS > 1) {
+        const int j = t + k * TP;
+        const int kk = j % NS;
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], tw[kk * r * (N / (NS * R))]);
+      }
+      Dft<R, S, T>::run(&v[k * R]);
+    }
+  }
+
+  // write pass outputs (Stockham positions) to LDS and read the next pass inputs
+  template <int R, int NS, int RN>
+  __device__ static void exchange(cx<T> (&v)[E], cx<T>* line, int t) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E / R; ++k) {
+      const int j = t + k * TP;
+      const int kk = j % NS;
+      const int base = (j - kk) * R + kk;
+#pragma unroll
+      for (int r = 0; r < R; ++r) line[pad_index<T>(base + r * NS)] = v[k * R + r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E / RN; ++k) {
+      const int j = t + k * TP;
+#pragma unroll
+      for (int r = 0; r < RN; ++r) v[k * RN + r] = line[pad_index<T>(j + r * (N / RN))];
+    }
+  }
+
+  template <class Load>
+  __device__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<T>* __restrict__ tw,
+                                   Load load, int b, int t) {
+    cx<T>* line = lds + b * LS;
+#pragma unroll
+    for (int k = 0; k < E / Sh::R0; ++k) {
+      const int j = t + k * TP;
+#pragma unroll
+      for (int r = 0; r < Sh::R0; ++r) {
+        if constexpr (std::is_same<Load, NoLoad>::value)
+          v[k * Sh::R0 + r] = line[pad_index<T>(j + r * (N / Sh::R0))];
+        else
+          v[k * Sh::R0 + r] = load(b, j + r * (N / Sh::R0));
+      }
+    }
+    compute<Sh::R0, 1>(v, t, tw);
+    if constexpr (Sh::R1 > 1) {
+      exchange<Sh::R0, 1, Sh::R1>(v, line, t);
+      compute<Sh::R1, Sh::R0>(v, t, tw);
+    }
+    if constexpr (Sh::R2 > 1) {
+      exchange<Sh::R1, Sh::R0, Sh::R2>(v, line, t);
+      compute<Sh::R2, Sh::R0 * Sh::R1>(v, t, tw);
+    }
+  }
+
+  // Result delivered to store(b, pos, value); stores of a lane are at
+  // pos = t + k*TP + r*N/RL (consecutive lanes -> consecutive positions).
+  template <class Load, class Store>
+  __device__ static void run(cx<T>* lds, const cx<T>* __restrict__ tw, Load load, Store store) {
+    const int b = threadIdx.x / TP, t = threadIdx.x % TP;
+    cx<T> v[E];
+    transform(v, lds, tw, load, b, t);
+#pragma unroll
+    for (int k = 0; k < E / RL; ++k) {
+      const int j = t + k * TP;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) store(b, j + r * (N / RL), v[k * RL + r]);
+    }
+  }
+
+  // Result left in LDS at out_at(b, pos); ends with a barrier.
+  template <class Load>
+  __device__ static void run_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Load load) {
+    const int b = threadIdx.x / TP, t = threadIdx.x % TP;
+    cx<T> v[E];
+    transform(v, lds, tw, load, b, t);
+    __syncthreads();
+    cx<T>* line = lds + b * LS;
+#pragma unroll
+    for (int k = 0; k < E / RL; ++k) {
+      const int j = t + k * TP;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) line[pad_index<T>(j + r * (N / RL))] = v[k * RL + r];
+    }
+    __syncthreads();
+  }
+};
+
+// ---------------------------------------------------------------- RT engine
+struct RtPlan {
+  int n;       // length
+  int np;      // number of passes
+  int ls;      // line stride (elements)
+  int lines;   // lines per block
+  int radix[16];
+};
+
+template <typename T, int S>
+struct FftRT {
+  __device__ static int in_at(const RtPlan& p, int b, int pos) { return b * p.ls + pos; }
+
+  template <int R>
+  __device__ static void pass(const RtPlan& p, const cx<T>* src, cx<T>* dst, int ns,
+                              const cx<T>* __restrict__ tw) {
+    const int nb = p.n / R;
+    const int twStride = p.n / (ns * R);
+    const int total = p.lines * nb;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int b = idx / nb, j = idx - b * nb;
+      const int kk = j % ns;
+      const cx<T>* s = src + b * p.ls;
+      cx<T> v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = s[j + r * nb];
+      if (kk) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = twm<S>(v[r], tw[kk * r * twStride]);
+      }
+      Dft<R, S, T>::run(v);
+      cx<T>* d = dst + b * p.ls + (j - kk) * R + kk;
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r * ns] = v[r];
+    }
+  }
+
+  __device__ static void pass_generic(const RtPlan& p, const cx<T>* src, cx<T>* dst, int ns,
+                                      int R, const cx<T>* __restrict__ tw) {
+    const int nb = p.n / R;
+    const int twStride = p.n / (ns * R);
+    const int dftStride = p.n / R;
+    const int total = p.lines * nb * R;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int q = idx % R;
+      const int rest = idx / R;
+      const int b = rest / nb, j = rest - b * nb;
+      const int kk = j % ns;
+      const cx<T>* s = src + b * p.ls;
+      cx<T> acc = s[j];
+      for (int r = 1; r < R; ++r) {
+        cx<T> x = s[j + r * nb];
+        if (kk) x = twm<S>(x, tw[static_cast<long long>(kk) * r * twStride]);
+        const int e = static_cast<int>((static_cast<long long>(r) * q) % R);
+        acc = acc + twm<S>(x, tw[e * dftStride]);
+      }
+      dst[b * p.ls + (j - kk) * R + kk + q * ns] = acc;
+    }
+  }
+
+  // Input in region 0 at in_at(b, pos); returns the region holding the result
+  // (index b*ls + pos). Ends with a barrier.
+  __device__ static cx<T>* run_in_lds(const RtPlan& p, cx<T>* lds, const cx<T>* __restrict__ tw) {
+    cx<T>* src = lds;
+    cx<T>* dst = lds + p.lines * p.ls;
+    int ns = 1;
+    for (int i = 0; i < p.np; ++i) {
+      const int R = p.radix[i];
+      switch (R) {
+        case 2: pass<2>(p, src, dst, ns, tw); break;
+        case 3: pass<3>(p, src, dst, ns, tw); break;
+        case 4: pass<4>(p, src, dst, ns, tw); break;
+        case 5: pass<5>(p, src, dst, ns, tw); break;
+        case 7: pass<7>(p, src, dst, ns, tw); break;
+        case 8: pass<8>(p, src, dst, ns, tw); break;
+        case 9: pass<9>(p, src, dst, ns, tw); break;
+        case 11: pass<11>(p, src, dst, ns, tw); break;
+        case 13: pass<13>(p, src, dst, ns, tw); break;
+        case 16: pass<16>(p, src, dst, ns, tw); break;
+        default: pass_generic(p, src, dst, ns, R, tw); break;
+      }
+      __syncthreads();
+      ns *= R;
+      cx<T>* tmp = src;
+      src = dst;
+      dst = tmp;
+    }
+    return src;
+  }
+};
+
+}  // namespace dev
+}  // namespace spfft

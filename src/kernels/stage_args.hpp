@@ -1,0 +1,82 @@
+// Kernel-argument structures and host launch entry points of the fused stage
+// kernels. One kernel per stage and direction:
+//   z stage: sparse values <-> z-sticks, z-FFT, (0,0)-stick hermitian fill,
+//            pack into the per-rank exchange layout (replaces K4-K6, K8, K9,
+//            K11, K13, K15 and the vendor z-FFT F1 of the reference).
+//   y stage: exchange layout <-> [z][column][y] slab, y-FFT over x-columns that
+//            hold sticks only, x=0 plane hermitian fill (replaces K2, K3, K7,
+//            K10, K12, K14, K16 and half of F2/F3).
+//   x stage: [z][column][y] <-> space domain [z][y][x], x-FFT C2C, C2R or R2C
+//            (replaces the other half of F2/F3).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "fft/codelets.hpp"
+#include "plan/index_plan.hpp"
+
+namespace spfft {
+namespace dev {
+
+struct ZArgs {
+  int numSticks;
+  int n;          // dimZ
+  int zeroStick;  // line to hermitian-fill (R2C backward), -1 for none
+  const StickRun* runs;
+  const int* runOffsets;
+  int single;                // 1: exchange side is the plain [S][n] array
+  const int* zRank;          // n entries: rank owning plane z
+  const long long* segDispl; // per rank
+  const long long* segStride;
+  const int* segZOff;
+};
+
+struct YArgs {
+  int ncols;
+  int L;  // local planes
+  int n;  // dimY
+  int colOfX0;  // column needing the x=0 plane hermitian fill, -1 for none
+  const int* colOffsets;
+  const int* colY;
+  const long long* colBase;
+};
+
+struct XArgs {
+  int L;
+  int Y;
+  int n;      // dimX
+  int nFreq;  // dimX/2+1 for R2C, dimX for C2C
+  int ncols;
+  const int* colX;
+};
+
+// Host launchers. `tw` is the length-n twiddle table exp(-2 pi i m / n).
+// BT is the exchange element type (cx<T> or cx<float> for *_FLOAT exchanges).
+template <typename T, typename BT>
+void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>* tw,
+                       hipStream_t stream);
+template <typename T, typename BT>
+void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, const cx<T>* tw,
+                      hipStream_t stream);
+template <typename T, typename BT>
+void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* tw,
+                       hipStream_t stream);
+template <typename T, typename BT>
+void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* tw,
+                      hipStream_t stream);
+template <typename T>
+void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space, const cx<T>* tw,
+                       hipStream_t stream);
+template <typename T>
+void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter, const cx<T>* tw,
+                      hipStream_t stream);
+
+// Largest run-time FFT length supported in one workgroup (LDS-resident).
+int max_device_fft_length(bool doublePrecision);
+// true if n has a compile-time (register-resident) kernel.
+bool has_ct_kernel(int n);
+
+}  // namespace dev
+}  // namespace spfft

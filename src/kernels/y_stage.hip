@@ -1,0 +1,47 @@
+// y-stage launchers: exchange layout <-> [z][column][y] with the y-FFT.
+#include "kernels/stage_kernels.hpp"
+
+namespace spfft {
+namespace dev {
+
+template <typename T, typename BT>
+void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* tw,
+                       hipStream_t stream) {
+  if (a.ncols <= 0 || a.L <= 0) return;
+  with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
+    auto k = y_backward_kernel<decltype(eng), T, BT>;
+    prepare_kernel(k, lds);
+    hipLaunchKernelGGL(k, dim3(a.ncols, ceil_div(a.L, lines)), dim3(threads), lds, stream, eng, a,
+                       in, inter, tw);
+    gpu_check_launch("y_backward", stream);
+  });
+}
+
+template <typename T, typename BT>
+void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* tw,
+                      hipStream_t stream) {
+  if (a.ncols <= 0 || a.L <= 0) return;
+  with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
+    auto k = y_forward_kernel<decltype(eng), T, BT>;
+    prepare_kernel(k, lds);
+    hipLaunchKernelGGL(k, dim3(a.ncols, ceil_div(a.L, lines)), dim3(threads), lds, stream, eng, a,
+                       inter, out, tw);
+    gpu_check_launch("y_forward", stream);
+  });
+}
+
+template void launch_y_backward<double, cx<double>>(const YArgs&, const cx<double>*, cx<double>*,
+                                                    const cx<double>*, hipStream_t);
+template void launch_y_backward<double, cx<float>>(const YArgs&, const cx<float>*, cx<double>*,
+                                                   const cx<double>*, hipStream_t);
+template void launch_y_backward<float, cx<float>>(const YArgs&, const cx<float>*, cx<float>*,
+                                                  const cx<float>*, hipStream_t);
+template void launch_y_forward<double, cx<double>>(const YArgs&, const cx<double>*, cx<double>*,
+                                                   const cx<double>*, hipStream_t);
+template void launch_y_forward<double, cx<float>>(const YArgs&, const cx<double>*, cx<float>*,
+                                                  const cx<double>*, hipStream_t);
+template void launch_y_forward<float, cx<float>>(const YArgs&, const cx<float>*, cx<float>*,
+                                                 const cx<float>*, hipStream_t);
+
+}  // namespace dev
+}  // namespace spfft

@@ -1,0 +1,201 @@
+"""GPU numerics: the hand-written HIP stage kernels against fp64 references
+(numpy for small sizes, torch.fft on the GPU for large ones)."""
+import numpy as np
+import pytest
+
+import spfft_amd as sp
+from spfft_amd.utils.indices import (center_indices, create_value_indices, sphere_indices)
+from spfft_amd.utils.oracle import dense_backward, dense_forward, max_rel_error
+
+pytestmark = pytest.mark.gpu
+
+GPU = sp.ProcessingUnit.GPU
+HOST = sp.ProcessingUnit.HOST
+
+
+def _rand_vals(rng, n, single=False):
+    v = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    return v.astype(np.complex64 if single else np.complex128)
+
+
+# lengths with a compile-time kernel (16..1024 powers of two) and run-time ones
+SIZES = [(2, 2, 2), (11, 12, 13), (16, 32, 64), (100, 13, 12), (1, 1, 7), (128, 1, 256),
+         (64, 100, 16), (13, 256, 1), (512, 3, 5), (36, 40, 45)]
+
+
+@pytest.mark.parametrize("dims", SIZES)
+@pytest.mark.parametrize("centered", [False, True])
+def test_c2c_sweep(gpu, dims, centered):
+    import torch
+    rng = np.random.default_rng(7)
+    nx, ny, nz = dims
+    idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+    if centered:
+        idx = center_indices(dims, [idx])[0]
+    vals = _rand_vals(rng, len(idx))
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    ref = dense_backward(idx, vals, dims)
+    dv = torch.as_tensor(vals, device=gpu)
+    for _ in range(2):  # twice: catches missing zero-fill (reference test_transform.hpp:129-131)
+        out = t.backward(dv)
+        assert max_rel_error(out.cpu().numpy(), ref) < 1e-12
+    space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < 1e-12
+
+
+@pytest.mark.parametrize("dims", [(8, 8, 8), (11, 12, 13), (16, 16, 32), (12, 11, 4), (2, 13, 11),
+                                  (256, 16, 16), (15, 64, 128)])
+def test_r2c(gpu, dims):
+    import torch
+    rng = np.random.default_rng(3)
+    nx, ny, nz = dims
+    space = rng.standard_normal((nz, ny, nx))
+    idx = create_value_indices(rng, [1.0], 1.0, 1.0, nx, ny, nz, True)[0]
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C, nx, ny, nz, nz, idx)
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < 1e-12
+    out = t.backward(f)
+    assert max_rel_error(out.cpu().numpy(), space * (nx * ny * nz)) < 1e-12
+
+
+def test_r2c_half_plane_symmetry(gpu):
+    """Only half of the x=0 plane / (0,0) stick given: hermitian fill on the GPU."""
+    import torch
+    rng = np.random.default_rng(5)
+    dims = (12, 10, 14)
+    nx, ny, nz = dims
+    space = rng.standard_normal((nz, ny, nx))
+    idx = create_value_indices(rng, [1.0], 1.0, 1.0, nx, ny, nz, True)[0]
+    # keep the x = 0 plane only for y <= ny/2 and the (0,0) stick only for z <= nz/2 (generator does)
+    vals = dense_forward(space, idx, dims)
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C, nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    ref = dense_backward(idx, vals, dims, r2c=True)
+    assert max_rel_error(out.cpu().numpy(), ref) < 1e-12
+    assert max_rel_error(out.cpu().numpy(), space * nx * ny * nz) < 1e-12
+
+
+@pytest.mark.parametrize("n", [64, 128])
+def test_sphere_c2c_large(gpu, n):
+    """Config 2 of BASELINE.json: n^3 C2C spherical cutoff, fp64, checked with torch.fft."""
+    import torch
+    dims = (n, n, n)
+    idx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(11)
+    vals = _rand_vals(rng, len(idx))
+    grid = sp.Grid(n, n, n, n * n, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, n, n, n, n, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    s = torch.as_tensor(np.where(idx < 0, idx + n, idx).astype(np.int64), device=gpu)
+    F = torch.zeros((n, n, n), dtype=torch.complex128, device=gpu)
+    F[s[:, 0], s[:, 1], s[:, 2]] = torch.as_tensor(vals, device=gpu)
+    ref = torch.fft.ifftn(F) * (n ** 3)
+    ref = ref.permute(2, 1, 0)
+    err = (out - ref).abs().max() / ref.abs().max()
+    assert err.item() < 1e-12
+    f = t.forward(None, scaling=sp.Scaling.FULL)
+    assert (f.cpu() - torch.as_tensor(vals)).abs().max().item() < 1e-12 * np.abs(vals).max() * 10
+
+
+@pytest.mark.parametrize("dims", [(11, 12, 13), (32, 32, 32), (64, 16, 36)])
+def test_single_precision(gpu, dims):
+    import torch
+    rng = np.random.default_rng(2)
+    nx, ny, nz = dims
+    idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+    vals = _rand_vals(rng, len(idx), single=True)
+    grid = sp.GridFloat(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    ref = dense_backward(idx, vals.astype(np.complex128), dims)
+    assert max_rel_error(out.cpu().numpy(), ref) < 2e-5
+
+
+def test_host_pointers_on_gpu_transform(gpu):
+    """GPU transform with host input/output and host space domain (staging paths)."""
+    rng = np.random.default_rng(4)
+    dims = (16, 12, 20)
+    nx, ny, nz = dims
+    idx = create_value_indices(rng, [1.0], 0.8, 0.8, nx, ny, nz, False)[0]
+    vals = _rand_vals(rng, len(idx))
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    out = t.backward(vals, HOST)
+    assert isinstance(out, np.ndarray)
+    assert max_rel_error(out, dense_backward(idx, vals, dims)) < 1e-12
+    res = np.empty(len(idx), dtype=np.complex128)
+    t.forward(None, output=res, input_location=HOST, scaling=sp.Scaling.FULL)
+    assert max_rel_error(res, vals) < 1e-12
+
+
+@pytest.mark.parametrize("exchange", list(sp.ExchangeType))
+def test_gpu_virtual_ranks(gpu, exchange):
+    """P virtual ranks on one GPU (in-process group, peer-copy data plane) through the
+    distributed pack/unpack layouts of every exchange type."""
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    dims = (24, 20, 18)
+    gidx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(9)
+    vals = _rand_vals(rng, len(gidx))
+    ref = dense_backward(gidx, vals, dims)
+    P = 3
+    parts = distribute_sticks(gidx, P, dims)
+    tol = 1e-6 if exchange in (sp.ExchangeType.BUFFERED_FLOAT,
+                               sp.ExchangeType.COMPACT_BUFFERED_FLOAT) else 1e-12
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU, exchange_type=exchange)
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.as_tensor(vals[start:start + len(s.indices)], device="cuda")
+        out = s.transform.backward(v).cpu().numpy()
+        e1 = max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length])
+        f = s.transform.forward(None, scaling=sp.Scaling.FULL).cpu().numpy()
+        e2 = max_rel_error(f, v.cpu().numpy())
+        return e1, e2
+
+    for e1, e2 in run_ranks(P, body):
+        assert e1 < tol and e2 < tol
+
+
+def test_multi_transform_gpu(gpu):
+    import torch
+    rng = np.random.default_rng(12)
+    dims = (32, 24, 20)
+    nx, ny, nz = dims
+    idx = sphere_indices(*dims, 0.5)
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t0 = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    ts = [t0, t0.clone(), t0.clone()]
+    vals = [_rand_vals(rng, len(idx)) for _ in ts]
+    outs = sp.multi_transform_backward(ts, [torch.as_tensor(v, device=gpu) for v in vals])
+    for o, v in zip(outs, vals):
+        assert max_rel_error(o.cpu().numpy(), dense_backward(idx, v, dims)) < 1e-12
+    res = sp.multi_transform_forward(ts, scalings=[sp.Scaling.FULL] * 3)
+    for r, v in zip(res, vals):
+        assert max_rel_error(r.cpu().numpy(), v) < 1e-12
+    with pytest.raises(sp.InvalidParameterError):
+        sp.multi_transform_backward([t0, t0], [vals[0], vals[0]])
+
+
+def test_user_stream_async(gpu):
+    import torch
+    rng = np.random.default_rng(13)
+    dims = (64, 64, 64)
+    idx = sphere_indices(*dims, 0.4)
+    vals = torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu)
+    grid = sp.Grid(*dims, 64 * 64, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, *dims, 64, idx)
+    s = torch.cuda.Stream()
+    t.set_stream(s, synchronous=False)
+    with torch.cuda.stream(s):
+        t.backward(vals)
+        out = t.forward(None, scaling=sp.Scaling.FULL)
+    t.synchronize()
+    assert (out - vals).abs().max().item() < 1e-12

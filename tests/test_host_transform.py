@@ -1,0 +1,87 @@
+"""Host (CPU) engine numerics against numpy — the SpFFT local test sweep
+(reference: tests/local_tests/test_local_transform.cpp, sizes {1,2,11,12,13,100})."""
+import itertools
+
+import numpy as np
+import pytest
+
+import spfft_amd as sp
+from spfft_amd.utils.indices import center_indices, create_value_indices
+from spfft_amd.utils.oracle import dense_backward, dense_forward, max_rel_error
+
+HOST = sp.ProcessingUnit.HOST
+SIZES = [1, 2, 11, 12, 13, 100]
+# a deterministic cover of the 216 combinations: every size in every axis, both sides
+COMBOS = sorted(set([(a, b, c) for a, b, c in itertools.product(SIZES, SIZES, SIZES)
+                     if (a * 7 + b * 3 + c) % 9 == 0 or len({a, b, c}) == 1]))
+
+
+@pytest.mark.parametrize("dims", COMBOS)
+@pytest.mark.parametrize("centered", [False, True])
+def test_c2c(dims, centered):
+    nx, ny, nz = dims
+    if nx * ny * nz > 200_000:
+        pytest.skip("large dense oracle")
+    rng = np.random.default_rng(42)
+    idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+    if centered:
+        idx = center_indices(dims, [idx])[0]
+    vals = rng.standard_normal(len(idx)) + 1j * rng.standard_normal(len(idx))
+    grid = sp.Grid(nx, ny, nz, nx * ny, HOST, 2)
+    t = grid.create_transform(HOST, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    ref = dense_backward(idx, vals, dims)
+    for _ in range(2):
+        out = t.backward(vals)
+        assert max_rel_error(out, ref) < 1e-12
+    space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+    f = t.forward(space)
+    assert max_rel_error(f, dense_forward(space, idx, dims)) < 1e-12
+    fs = t.forward(space, scaling=sp.Scaling.FULL)
+    assert max_rel_error(fs, dense_forward(space, idx, dims, scale=True)) < 1e-12
+
+
+@pytest.mark.parametrize("dims", [(1, 1, 1), (2, 2, 2), (11, 12, 13), (12, 11, 13), (13, 13, 2),
+                                  (100, 11, 2), (2, 100, 12), (12, 12, 100)])
+@pytest.mark.parametrize("centered", [False, True])
+def test_r2c(dims, centered):
+    nx, ny, nz = dims
+    rng = np.random.default_rng(42)
+    space = rng.standard_normal((nz, ny, nx))
+    idx = create_value_indices(rng, [1.0], 1.0, 1.0, nx, ny, nz, True)[0]
+    if centered:
+        # x stays non-negative for R2C (reference indices.hpp:137-141)
+        c = center_indices(dims, [idx])[0]
+        c[:, 0] = idx[:, 0]
+        idx = c
+    grid = sp.Grid(nx, ny, nz, nx * ny, HOST, 2)
+    t = grid.create_transform(HOST, sp.TransformType.R2C, nx, ny, nz, nz, idx)
+    f = t.forward(space)
+    assert max_rel_error(f, dense_forward(space, idx, dims)) < 1e-12
+    out = t.backward(f)
+    assert max_rel_error(out, space * nx * ny * nz) < 1e-12
+
+
+def test_readme_example_2x2x2():
+    """Config 1 of BASELINE.json: 2x2x2 C2C on SPFFT_PU_HOST (reference README example)."""
+    dims = (2, 2, 2)
+    idx = np.array([(x, y, z) for x in range(2) for y in range(2) for z in range(2)], np.int32)
+    vals = np.array([complex(i, -i) for i in range(8)])
+    grid = sp.Grid(2, 2, 2, 4, HOST, -1)
+    t = grid.create_transform(HOST, sp.TransformType.C2C, 2, 2, 2, 2, idx)
+    out = t.backward(vals)
+    assert max_rel_error(out, dense_backward(idx, vals, dims)) < 1e-14
+    back = t.forward(None, scaling=sp.Scaling.FULL)
+    assert max_rel_error(back, vals) < 1e-14
+
+
+def test_single_precision_host():
+    rng = np.random.default_rng(1)
+    dims = (12, 11, 13)
+    nx, ny, nz = dims
+    idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+    vals = (rng.standard_normal(len(idx)) + 1j * rng.standard_normal(len(idx))).astype(np.complex64)
+    grid = sp.GridFloat(nx, ny, nz, nx * ny, HOST, 2)
+    t = grid.create_transform(HOST, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    out = t.backward(vals)
+    assert out.dtype == np.complex64
+    assert max_rel_error(out, dense_backward(idx, vals, dims)) < 1e-5
