@@ -70,6 +70,14 @@ SPFFT_EXPORT SpfftError spfft_amd_float_transform_synchronize(SpfftFloatTransfor
 SPFFT_EXPORT SpfftError spfft_amd_transform_local_z_offset_rank(SpfftTransform transform, int rank,
                                                                 int* offset, int* length);
 
+/* Zero-copy DLPack export (DLManagedTensor*) of the space domain [localZ][Y][X];
+ * the tensor keeps the transform and its grid alive until its deleter runs. */
+SPFFT_EXPORT SpfftError spfft_amd_transform_space_domain_dlpack(SpfftTransform transform,
+                                                                SpfftProcessingUnitType location,
+                                                                void** managedTensor);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_space_domain_dlpack(
+    SpfftFloatTransform transform, SpfftProcessingUnitType location, void** managedTensor);
+
 /* Step-wise execution (forward: xy, exchange, z; backward: z, exchange, xy). */
 SPFFT_EXPORT SpfftError spfft_amd_transform_forward_xy(SpfftTransform t,
                                                        SpfftProcessingUnitType inputLocation);

@@ -38,6 +38,7 @@ def build(clean: bool = False, jobs: int | None = None, build_type: str = "Relea
               f"-DCMAKE_C_COMPILER={clang}/clang", f"-DCMAKE_CXX_COMPILER={clang}/clang++",
               f"-DCMAKE_HIP_COMPILER={clang}/clang++", "-DCMAKE_HIP_ARCHITECTURES=gfx950"], env=env)
     _run(["cmake", "--build", BUILD_DIR, "-j", str(jobs)], env=env)
+    _check_targets()
     os.makedirs(NATIVE_DIR, exist_ok=True)
     for so in glob.glob(os.path.join(BUILD_DIR, "libspfft_amd*.so*")):
         if os.path.islink(so):
@@ -52,6 +53,22 @@ def build(clean: bool = False, jobs: int | None = None, build_type: str = "Relea
         if os.path.exists(src):
             shutil.copy2(src, os.path.join(NATIVE_DIR, exe))
     return NATIVE_DIR
+
+
+def _check_targets():
+    """Every kernel object must carry a gfx950 code object (and nothing else)."""
+    objs = glob.glob(os.path.join(BUILD_DIR, "CMakeFiles", "spfft_amd.dir", "src", "kernels", "*.o"))
+    llvm = os.path.join(ROCM, "llvm", "bin")
+    for o in objs:
+        tmp = o + ".fatbin"
+        subprocess.run([os.path.join(llvm, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + tmp, o],
+                       check=True)
+        out = subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--list", "--type=o",
+                              "--input=" + tmp], check=True, capture_output=True, text=True).stdout
+        os.remove(tmp)
+        gpus = [l for l in out.split() if "amdgcn" in l]
+        if not gpus or any(not l.endswith("gfx950") for l in gpus):
+            raise RuntimeError(f"{o}: unexpected offload targets {gpus}")
 
 
 def main(argv=None):

@@ -21,6 +21,20 @@ except Exception:  # pragma: no cover
     torch = None
 
 
+_SHUTDOWN = [False]
+
+
+def _at_exit():
+    # objects still alive at interpreter exit are not destroyed through the native
+    # library: the HIP runtime may already be tearing down.
+    _SHUTDOWN[0] = True
+
+
+import atexit  # noqa: E402
+
+atexit.register(_at_exit)
+
+
 def _check(code: int) -> None:
     if code != 0:
         msg = lib().spfft_amd_last_error_message()
@@ -106,7 +120,7 @@ class _GridBase:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and not _SHUTDOWN[0]:
             try:
                 self._prec.fn("grid_destroy")(h)
             except Exception:
@@ -177,7 +191,7 @@ class _TransformBase:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and not _SHUTDOWN[0]:
             try:
                 self._prec.fn("transform_destroy")(h)
             except Exception:
@@ -241,10 +255,11 @@ class _TransformBase:
             buf._owner = self  # the view keeps the transform (and its grid) alive
             arr = np.frombuffer(buf, dtype=dtype).reshape(shape)
             return arr
-        from .ops._dlpack import kDLComplex, kDLFloat, kDLROCM, to_torch
-        bits = (32 if self._single else 64) * (1 if real else 2)
-        return to_torch(ptr, shape, kDLFloat if real else kDLComplex, bits, kDLROCM,
-                        self.device_id, self)
+        from .ops._dlpack import capsule_to_torch
+        m = ctypes.c_void_p()
+        _check(self._prec.amd_fn("transform_space_domain_dlpack")(self._h, int(location),
+                                                                  ctypes.byref(m)))
+        return capsule_to_torch(m.value)
 
     def _default_output(self):
         n = self.num_local_elements

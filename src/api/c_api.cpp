@@ -69,6 +69,66 @@ SpfftError with_handle(void* h, F&& f) {
 
 using CommHandle = std::shared_ptr<Communicator>;
 
+// Minimal DLPack (v0.8 ABI) structures for zero-copy export of the space domain.
+struct DLDeviceX {
+  int32_t device_type;  // 1 = CPU, 10 = ROCm
+  int32_t device_id;
+};
+struct DLDataTypeX {
+  uint8_t code;  // 2 = float, 5 = complex
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensorX {
+  void* data;
+  DLDeviceX device;
+  int32_t ndim;
+  DLDataTypeX dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensorX {
+  DLTensorX dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensorX*);
+};
+
+template <typename TR>
+struct DlpackHolder {
+  DLManagedTensorX managed;
+  int64_t shape[3];
+  TR owner;  // shares the transform (and its grid) until torch drops the view
+};
+
+template <typename TR>
+void dlpack_delete(DLManagedTensorX* m) {
+  delete static_cast<DlpackHolder<TR>*>(m->manager_ctx);
+}
+
+template <typename TR, typename T>
+void* export_space_domain(TR& t, SpfftProcessingUnitType loc) {
+  auto* h = new DlpackHolder<TR>{DLManagedTensorX{}, {0, 0, 0}, t};
+  const bool real = t.type() == SPFFT_TRANS_R2C;
+  h->shape[0] = t.local_z_length();
+  h->shape[1] = t.dim_y();
+  h->shape[2] = t.dim_x();
+  DLTensorX& d = h->managed.dl_tensor;
+  d.data = t.space_domain_data(loc);
+  d.device.device_type = loc == SPFFT_PU_GPU ? 10 : 1;
+  d.device.device_id = loc == SPFFT_PU_GPU ? t.device_id() : 0;
+  d.ndim = 3;
+  d.dtype.code = real ? 2 : 5;
+  d.dtype.bits = static_cast<uint8_t>(sizeof(T) * 8 * (real ? 1 : 2));
+  d.dtype.lanes = 1;
+  d.shape = h->shape;
+  d.strides = nullptr;
+  d.byte_offset = 0;
+  h->managed.manager_ctx = h;
+  h->managed.deleter = &dlpack_delete<TR>;
+  return &h->managed;
+}
+
 }  // namespace
 
 extern "C" {
@@ -305,6 +365,21 @@ SpfftError spfft_amd_transform_local_z_offset_rank(SpfftTransform t, int rank, i
     if (rank < 0 || rank >= p.size) throw InvalidParameterError();
     *offset = p.planeOffsets[rank];
     *length = p.planesPerRank[rank];
+  });
+}
+
+SpfftError spfft_amd_transform_space_domain_dlpack(SpfftTransform t, SpfftProcessingUnitType loc,
+                                                   void** managedTensor) {
+  if (!managedTensor) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<Transform>(
+      t, [&](Transform& x) { *managedTensor = export_space_domain<Transform, double>(x, loc); });
+}
+SpfftError spfft_amd_float_transform_space_domain_dlpack(SpfftFloatTransform t,
+                                                         SpfftProcessingUnitType loc,
+                                                         void** managedTensor) {
+  if (!managedTensor) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) {
+    *managedTensor = export_space_domain<TransformFloat, float>(x, loc);
   });
 }
 

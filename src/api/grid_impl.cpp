@@ -115,7 +115,7 @@ GridImpl<T>::GridImpl(const GridImpl& o)
 
 template <typename T>
 GridImpl<T>::~GridImpl() {
-  if (pu_ & SPFFT_PU_GPU) {
+  if ((pu_ & SPFFT_PU_GPU) && !process_exiting()) {
     // release device resources on the grid's device
     try {
       DeviceGuard guard(deviceId_);

@@ -32,7 +32,7 @@ public:
     nccl_check(ncclCommInitRank(&nccl_, size_, all[0], rank_));
   }
   ~RcclDeviceComm() override {
-    if (nccl_) (void)ncclCommDestroy(nccl_);
+    if (nccl_ && !process_exiting()) (void)ncclCommDestroy(nccl_);
   }
 
   void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,

@@ -76,6 +76,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
 
 template <typename T>
 GpuExecutor<T>::~GpuExecutor() {
+  if (process_exiting()) return;
   try {
     DeviceGuard guard(deviceId_);
     if (stream_) (void)hipStreamSynchronize(stream_);

@@ -1,11 +1,21 @@
 #include "gpu/gpu_runtime.hpp"
 
+#include <atomic>
 #include <cstdlib>
 #include <string>
 
 #include "core/host_buffer.hpp"
 
 namespace spfft {
+
+namespace {
+std::atomic<bool> gExiting{false};
+struct ExitHook {
+  ExitHook() { std::atexit([] { gExiting.store(true); }); }
+} gExitHook;
+}  // namespace
+
+bool process_exiting() { return gExiting.load(); }
 
 void throw_gpu_error(hipError_t err, const char* /*what*/) {
   switch (err) {
@@ -53,12 +63,12 @@ DeviceGuard::~DeviceGuard() {
 
 GpuStream::GpuStream() { gpu_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"); }
 GpuStream::~GpuStream() {
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_ && !process_exiting()) (void)hipStreamDestroy(stream_);
 }
 
 GpuEvent::GpuEvent() { gpu_check(hipEventCreateWithFlags(&event_, hipEventDisableTiming), "hipEventCreate"); }
 GpuEvent::~GpuEvent() {
-  if (event_) (void)hipEventDestroy(event_);
+  if (event_ && !process_exiting()) (void)hipEventDestroy(event_);
 }
 
 DeviceBuffer::DeviceBuffer(std::size_t bytes) : bytes_(bytes) {
@@ -73,7 +83,7 @@ DeviceBuffer::DeviceBuffer(std::size_t bytes) : bytes_(bytes) {
 }
 
 DeviceBuffer::~DeviceBuffer() {
-  if (ptr_) (void)hipFree(ptr_);
+  if (ptr_ && !process_exiting()) (void)hipFree(ptr_);
 }
 
 bool is_device_pointer(const void* ptr) {
@@ -106,6 +116,8 @@ bool gpu_host_register(void* ptr, std::size_t bytes) {
   return true;
 }
 
-void gpu_host_unregister(void* ptr) { (void)hipHostUnregister(ptr); }
+void gpu_host_unregister(void* ptr) {
+  if (!process_exiting()) (void)hipHostUnregister(ptr);
+}
 
 }  // namespace spfft

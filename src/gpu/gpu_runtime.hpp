@@ -79,6 +79,11 @@ private:
   std::size_t bytes_ = 0;
 };
 
+// True once the process is exiting (atexit): destructors then leave GPU
+// resources to the driver instead of calling into a runtime that may already be
+// tearing down.
+bool process_exiting();
+
 // true if ptr is device (or managed) memory accessible by the GPU kernels.
 bool is_device_pointer(const void* ptr);
 int current_device();
