@@ -44,6 +44,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   // device tables (uploaded once; the hot path never touches the host plan)
   upload(runs_, p.runs);
   upload(runOffsets_, p.stickRunOffsets);
+  if (p.simpleSticks) upload(descs_, p.stickDescs);
   std::vector<int> zRank(p.dimZ, 0);
   for (int r = 0; r < p.size; ++r)
     for (int z = 0; z < p.planesPerRank[r]; ++z) zRank[p.planeOffsets[r] + z] = r;
@@ -137,6 +138,7 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
   a.zeroStick = p.type == SPFFT_TRANS_R2C ? p.zeroStick : -1;
   a.runs = runs_ ? runs_->data<StickRun>() : nullptr;
   a.runOffsets = runOffsets_ ? runOffsets_->data<int>() : nullptr;
+  a.desc = descs_ ? descs_->data<StickDesc>() : nullptr;
   a.single = p.size == 1 ? 1 : 0;
   a.zRank = zRank_ ? zRank_->data<int>() : nullptr;
   a.segDispl = segDispl_ ? segDispl_->data<long long>() : nullptr;

@@ -58,7 +58,7 @@ private:
   std::unique_ptr<GpuEvent> event_;
 
   // device tables
-  std::unique_ptr<DeviceBuffer> runs_, runOffsets_, zRank_, segDispl_, segStride_, segZOff_;
+  std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_, zRank_, segDispl_, segStride_, segZOff_;
   std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
   std::unique_ptr<DeviceBuffer> twX_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;

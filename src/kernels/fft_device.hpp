@@ -98,13 +98,25 @@ struct CtShape<1024> {
 
 struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 
-template <typename T, int N, int S>
+// largest power of two <= b, at most 16 (line-fast lane mapping)
+__host__ __device__ constexpr int lf_lines(int b) {
+  int p = 1;
+  while (p * 2 <= b && p * 2 <= 16) p *= 2;
+  return p;
+}
+
+// LF (line-fast) selects the lane -> (line b, lane t) mapping:
+//  false: t fastest (a line's TP lanes adjacent; row-contiguous global access),
+//  true:  b fastest (B lines adjacent; column-contiguous global access, e.g. a
+//         stick's z-run or an intermediate column's y-run).
+template <typename T, int N, int S, bool LF = false>
 struct FftCT {
   using Sh = CtShape<N>;
   static constexpr int E = Sh::E;
   static constexpr int TP = N / E;  // lanes per line
   static constexpr int LS = padded_stride<T>(N);
-  static constexpr int B = lines_per_block(TP, LS * static_cast<int>(sizeof(cx<T>)));
+  static constexpr int B0 = lines_per_block(TP, LS * static_cast<int>(sizeof(cx<T>)));
+  static constexpr int B = LF ? lf_lines(B0) : B0;
   static constexpr int NT = B * TP;
   static constexpr int RL = Sh::R2 > 1 ? Sh::R2 : (Sh::R1 > 1 ? Sh::R1 : Sh::R0);
 
@@ -179,9 +191,12 @@ struct FftCT {
 
   // Result delivered to store(b, pos, value); stores of a lane are at
   // pos = t + k*TP + r*N/RL (consecutive lanes -> consecutive positions).
+  __device__ static int lane_line() { return LF ? threadIdx.x % B : threadIdx.x / TP; }
+  __device__ static int lane_pos() { return LF ? threadIdx.x / B : threadIdx.x % TP; }
+
   template <class Load, class Store>
   __device__ static void run(cx<T>* lds, const cx<T>* __restrict__ tw, Load load, Store store) {
-    const int b = threadIdx.x / TP, t = threadIdx.x % TP;
+    const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
 #pragma unroll
@@ -195,7 +210,7 @@ struct FftCT {
   // Result left in LDS at out_at(b, pos); ends with a barrier.
   template <class Load>
   __device__ static void run_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Load load) {
-    const int b = threadIdx.x / TP, t = threadIdx.x % TP;
+    const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
     __syncthreads();

@@ -26,6 +26,7 @@ struct ZArgs {
   int zeroStick;  // line to hermitian-fill (R2C backward), -1 for none
   const StickRun* runs;
   const int* runOffsets;
+  const StickDesc* desc;     // non-null when every stick is simple (fast path)
   int single;                // 1: exchange side is the plain [S][n] array
   const int* zRank;          // n entries: rank owning plane z
   const long long* segDispl; // per rank

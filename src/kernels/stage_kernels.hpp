@@ -14,14 +14,15 @@ namespace spfft {
 namespace dev {
 
 // ------------------------------------------------------------ engine adapters
-template <typename T, int N, int S>
+template <typename T, int N, int S, bool LF = false>
 struct CtEng {
-  using F = FftCT<T, N, S>;
+  using F = FftCT<T, N, S, LF>;
   __device__ int lines() const { return F::B; }
   __device__ int n() const { return N; }
   __device__ int in_at(int b, int pos) const { return F::in_at(b, pos); }
   __device__ int out_at(int b, int pos) const { return F::out_at(b, pos); }
   __device__ int input_elems() const { return F::B * F::LS; }
+  __device__ int lds_bytes() const { return static_cast<int>(F::lds_bytes()); }
   template <class St>
   __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     F::run(lds, tw, NoLoad{}, st);
@@ -29,6 +30,13 @@ struct CtEng {
   template <class Ld>
   __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
     F::run_to_lds(lds, tw, ld);
+  }
+  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
+    F::run_to_lds(lds, tw, NoLoad{});
+  }
+  template <class Ld, class St>
+  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+    F::run(lds, tw, ld, st);
   }
   // host side
   static int h_lines() { return F::B; }
@@ -46,6 +54,9 @@ struct RtEng {
     return ((p.np & 1) ? p.lines * p.ls : 0) + b * p.ls + pos;
   }
   __device__ int input_elems() const { return p.lines * p.ls; }
+  __device__ int lds_bytes() const {
+    return 2 * p.lines * p.ls * static_cast<int>(sizeof(cx<T>));
+  }
   template <class St>
   __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     const cx<T>* res = FftRT<T, S>::run_in_lds(p, lds, tw);
@@ -64,6 +75,18 @@ struct RtEng {
     }
     __syncthreads();
     FftRT<T, S>::run_in_lds(p, lds, tw);
+  }
+  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
+    FftRT<T, S>::run_in_lds(p, lds, tw);
+  }
+  template <class Ld, class St>
+  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+    global_to_lds(lds, tw, ld);
+    const int total = p.lines * p.n;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int b = idx / p.n, pos = idx - b * p.n;
+      st(b, pos, lds[out_at(b, pos)]);
+    }
   }
 };
 
@@ -117,6 +140,133 @@ __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
   extern __shared__ __attribute__((aligned(16))) char spfftSmem[]; \
   cx<T>* lds = reinterpret_cast<cx<T>*>(spfftSmem)
 
+// Loads issued per lane before the first dependent LDS store: keeps U global
+// loads in flight per lane (memory-level parallelism for the gathers).
+constexpr int kGatherUnroll = 16;
+
+// for idx in [0, total): lds[dst(idx)] = load(idx) (dst < 0: skip), U loads in flight.
+template <typename T, class Load, class Dst>
+__device__ __forceinline__ void gather_to_lds(cx<T>* lds, int total, Load load, Dst dst) {
+  for (int base = threadIdx.x; base < total; base += blockDim.x * kGatherUnroll) {
+    cx<T> v[kGatherUnroll];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) v[u] = load(idx);
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) {
+        const int d = dst(idx);
+        if (d >= 0) lds[d] = v[u];
+      }
+    }
+  }
+}
+
+// Exclusive prefix sum of n ints in LDS (one wave, 64-wide shuffle scans); writes
+// out[0..n] (out[n] = total). Ends with a barrier.
+__device__ __forceinline__ void wave_exclusive_scan(const int* in, int* out, int n) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int carry = 0;
+    for (int c = 0; c < n; c += 64) {
+      const int i = c + lane;
+      const int v = i < n ? in[i] : 0;
+      int x = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      if (i < n) out[i] = carry + x - v;
+      carry += __shfl(x, 63, 64);
+    }
+    if (lane == 0) out[n] = carry;
+  }
+  __syncthreads();
+}
+
+// Run table of a block of sticks staged in LDS (after the FFT lines):
+// the gather/scatter between sparse values and sticks is then one flat loop
+// with all loads independent (value index = first + idx when the block's runs
+// are consecutive in value order, the common stick-major input).
+struct RunTable {
+  StickRun* runs;
+  int* start;  // exclusive prefix of run lengths, count+1 entries
+  int count;
+  int total;
+  bool contiguous;
+};
+
+constexpr int kRunsPerLine = 4;  // table capacity per stick line
+
+__host__ __device__ constexpr std::size_t run_table_bytes(int lines) {
+  return std::size_t(kRunsPerLine) * lines * (sizeof(StickRun) + sizeof(int)) + 16 >
+                 std::size_t(lines) * sizeof(StickDesc)
+             ? std::size_t(kRunsPerLine) * lines * (sizeof(StickRun) + sizeof(int)) + 16
+             : std::size_t(lines) * sizeof(StickDesc);
+}
+
+// Returns false if the block's runs do not fit the table (caller falls back).
+__device__ __forceinline__ bool load_run_table(const ZArgs& a, int s0, int lines, char* base,
+                                               RunTable& t) {
+  const int s1 = min(s0 + lines, a.numSticks);
+  const int q0 = a.runOffsets[s0];
+  const int q1 = a.runOffsets[s1];
+  const int R = q1 - q0;
+  if (R > kRunsPerLine * lines) return false;  // block-uniform
+  t.runs = reinterpret_cast<StickRun*>(base);
+  int* lens = reinterpret_cast<int*>(base + sizeof(StickRun) * kRunsPerLine * lines);
+  t.start = lens;  // scanned in place into a shifted copy below
+  int ok = 1;
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    const StickRun r = a.runs[q0 + i];
+    t.runs[i] = r;
+    if (i > 0) {
+      const StickRun p = a.runs[q0 + i - 1];
+      if (p.valueStart + p.length != r.valueStart) ok = 0;
+    }
+  }
+  t.contiguous = __syncthreads_and(ok) != 0;
+  // prefix of lengths (wave 0), lengths read from the staged runs
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int carry = 0;
+    for (int c = 0; c < R; c += 64) {
+      const int i = c + lane;
+      const int v = i < R ? t.runs[i].length : 0;
+      int x = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      if (i < R) lens[i] = carry + x - v;
+      carry += __shfl(x, 63, 64);
+    }
+    if (lane == 0) lens[R] = carry;
+  }
+  __syncthreads();
+  t.count = R;
+  t.total = lens[R];
+  return true;
+}
+
+// index of the run containing flat element idx (binary search over start[])
+__device__ __forceinline__ int find_run(const RunTable& t, int idx) {
+  int lo = 0, hi = t.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.start[mid] <= idx)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
 // ---------------------------------------------------------------- z stage
 template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(kMaxThreads)
@@ -126,17 +276,54 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int B = eng.lines();
   const int s0 = blockIdx.x * B;
   zero_lds(lds, eng.input_elems());
-  __syncthreads();
-  // decompress: one wave per stick, lanes stride the runs (coalesced value reads)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int b = wave; b < B; b += nw) {
-    const int s = s0 + b;
-    if (s >= a.numSticks) break;
-    const int q1 = a.runOffsets[s + 1];
-    for (int q = a.runOffsets[s]; q < q1; ++q) {
-      const StickRun r = a.runs[q];
-      for (int j = lane; j < r.length; j += 64)
-        lds[eng.in_at(b, r.zStart + j)] = values[r.valueStart + j];
+  RunTable tab;
+  char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
+  if (a.desc) {
+    // simple sticks: (line b, j) -> value desc.valueStart + j, z from the two runs
+    StickDesc* d = reinterpret_cast<StickDesc*>(tableBase);
+    const int nl = min(B, a.numSticks - s0);
+    for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
+    __syncthreads();
+    const int n = eng.n();
+    gather_to_lds(lds, nl * n, [&](int idx) {
+      const int b = idx / n, j = idx - b * n;
+      return j < d[b].count ? values[d[b].valueStart + j] : czero<T>();
+    }, [&](int idx) {
+      const int b = idx / n, j = idx - b * n;
+      const StickDesc& q = d[b];
+      if (j >= q.count) return -1;
+      return eng.in_at(b, j < q.len0 ? q.z0 + j : q.z1 + (j - q.len0));
+    });
+  } else if (load_run_table(a, s0, B, tableBase, tab)) {
+    // decompress: flat over the block's values, kGatherUnroll loads in flight per lane
+    if (tab.contiguous) {
+      const cx<T>* src = values + tab.runs[0].valueStart;
+      gather_to_lds(lds, tab.total, [&](int idx) { return src[idx]; }, [&](int idx) {
+        const int q = find_run(tab, idx);
+        return eng.in_at(tab.runs[q].stick - s0, tab.runs[q].zStart + idx - tab.start[q]);
+      });
+    } else {
+      gather_to_lds(lds, tab.total, [&](int idx) {
+        const int q = find_run(tab, idx);
+        return values[tab.runs[q].valueStart + idx - tab.start[q]];
+      }, [&](int idx) {
+        const int q = find_run(tab, idx);
+        return eng.in_at(tab.runs[q].stick - s0, tab.runs[q].zStart + idx - tab.start[q]);
+      });
+    }
+  } else {
+    // many short runs (unsorted input): one wave per stick
+    __syncthreads();  // zero-fill complete
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int b = wave; b < B; b += nw) {
+      const int s = s0 + b;
+      if (s >= a.numSticks) break;
+      const int q1 = a.runOffsets[s + 1];
+      for (int q = a.runOffsets[s]; q < q1; ++q) {
+        const StickRun r = a.runs[q];
+        for (int j = lane; j < r.length; j += 64)
+          lds[eng.in_at(b, r.zStart + j)] = values[r.valueStart + j];
+      }
     }
   }
   __syncthreads();
@@ -159,124 +346,202 @@ __global__ void __launch_bounds__(kMaxThreads)
     if (s >= a.numSticks) return czero<T>();
     return cvt<T>(in[seg_index(a, s, pos)]);
   });
-  // compress (+ scaling): one wave per stick
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int b = wave; b < B; b += nw) {
-    const int s = s0 + b;
-    if (s >= a.numSticks) break;
-    const int q1 = a.runOffsets[s + 1];
-    for (int q = a.runOffsets[s]; q < q1; ++q) {
-      const StickRun r = a.runs[q];
-      for (int j = lane; j < r.length; j += 64)
-        values[r.valueStart + j] = spfft::scale(lds[eng.out_at(b, r.zStart + j)], scale);
+  // compress (+ scaling)
+  RunTable tab;
+  char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
+  if (a.desc) {
+    StickDesc* d = reinterpret_cast<StickDesc*>(tableBase);
+    const int nl = min(B, a.numSticks - s0);
+    for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
+    __syncthreads();
+    const int n = eng.n();
+    for (int idx = threadIdx.x; idx < nl * n; idx += blockDim.x) {
+      const int b = idx / n, j = idx - b * n;
+      const StickDesc& q = d[b];
+      if (j < q.count) {
+        const int z = j < q.len0 ? q.z0 + j : q.z1 + (j - q.len0);
+        values[q.valueStart + j] = spfft::scale(lds[eng.out_at(b, z)], scale);
+      }
+    }
+  } else if (load_run_table(a, s0, B, tableBase, tab)) {
+    for (int idx = threadIdx.x; idx < tab.total; idx += blockDim.x) {
+      const int q = find_run(tab, idx);
+      const StickRun& r = tab.runs[q];
+      const int off = idx - tab.start[q];
+      values[r.valueStart + off] = spfft::scale(lds[eng.out_at(r.stick - s0, r.zStart + off)], scale);
+    }
+  } else {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int b = wave; b < B; b += nw) {
+      const int s = s0 + b;
+      if (s >= a.numSticks) break;
+      const int q1 = a.runOffsets[s + 1];
+      for (int q = a.runOffsets[s]; q < q1; ++q) {
+        const StickRun r = a.runs[q];
+        for (int j = lane; j < r.length; j += 64)
+          values[r.valueStart + j] = spfft::scale(lds[eng.out_at(b, r.zStart + j)], scale);
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------- y stage
+// Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
+// loads straight from the stick side — consecutive lanes read consecutive z
+// of one stick (coalesced) — with no LDS staging of the input. The x = 0
+// column of an R2C transform is gathered into LDS for the hermitian fill.
 template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(kMaxThreads)
     y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
+  const int n = eng.n();
   const int c = blockIdx.x;
   const int z0 = blockIdx.y * B;
-  zero_lds(lds, eng.input_elems());
-  __syncthreads();
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
-  for (int idx = threadIdx.x; idx < ne * B; idx += blockDim.x) {
-    const int e = idx / B, zz = idx - e * B;
-    if (z0 + zz < a.L) lds[eng.in_at(zz, a.colY[k0 + e])] = cvt<T>(in[a.colBase[k0 + e] + z0 + zz]);
+  long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  int* yEnt = reinterpret_cast<int*>(cBase + n);
+  int* cY = yEnt + n;
+  for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
+  __syncthreads();
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+    const int y = a.colY[k0 + e];
+    cBase[e] = a.colBase[k0 + e] + z0;
+    yEnt[y] = e;
+    cY[e] = y;
   }
   __syncthreads();
-  if (c == a.colOfX0) hermitian_lines(eng, lds, 0, B, a.n);
-  eng.lds_to_global(lds, tw, [&](int b, int pos, cx<T> v) {
-    const int z = z0 + b;
-    if (z < a.L) inter[(static_cast<long long>(z) * a.ncols + c) * a.n + pos] = v;
-  });
+  const int zl = min(B, a.L - z0);
+  if (c != a.colOfX0) {
+    eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
+      const int e = yEnt[pos];
+      if (e < 0 || b >= zl) return czero<T>();
+      return cvt<T>(in[cBase[e] + b]);
+    });
+  } else {
+    zero_lds(lds, eng.input_elems());
+    __syncthreads();
+    gather_to_lds(lds, ne * zl, [&](int idx) {
+      const int e = idx / zl, zz = idx - e * zl;
+      return cvt<T>(in[cBase[e] + zz]);
+    }, [&](int idx) {
+      const int e = idx / zl, zz = idx - e * zl;
+      return eng.in_at(zz, cY[e]);
+    });
+    __syncthreads();
+    hermitian_lines(eng, lds, 0, B, n);
+    eng.lds_to_lds(lds, tw);
+  }
+  // rows of [z][column][y] are contiguous: coalesced copy-out
+  for (int idx = threadIdx.x; idx < zl * n; idx += blockDim.x) {
+    const int b = idx / n, pos = idx - b * n;
+    inter[(static_cast<long long>(z0 + b) * a.ncols + c) * n + pos] = lds[eng.out_at(b, pos)];
+  }
 }
 
+// Forward y stage, line-fast engine: lanes read rows of the intermediate and
+// write each stick's z-run of this plane block directly (consecutive lanes ->
+// consecutive z of one stick); no LDS staging on either side.
 template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(kMaxThreads)
     y_forward_kernel(Eng eng, YArgs a, const cx<T>* __restrict__ inter, BT* __restrict__ out,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
+  const int n = eng.n();
   const int c = blockIdx.x;
   const int z0 = blockIdx.y * B;
-  eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
-    const int z = z0 + b;
-    if (z >= a.L) return czero<T>();
-    return inter[(static_cast<long long>(z) * a.ncols + c) * a.n + pos];
-  });
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
-  for (int idx = threadIdx.x; idx < ne * B; idx += blockDim.x) {
-    const int e = idx / B, zz = idx - e * B;
-    if (z0 + zz < a.L)
-      out[a.colBase[k0 + e] + z0 + zz] = cvt<typename BT::value_type>(lds[eng.out_at(zz, a.colY[k0 + e])]);
+  long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  int* yEnt = reinterpret_cast<int*>(cBase + n);
+  for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
+  __syncthreads();
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+    cBase[e] = a.colBase[k0 + e] + z0;
+    yEnt[a.colY[k0 + e]] = e;
   }
+  __syncthreads();
+  const int zl = min(B, a.L - z0);
+  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+    if (b >= zl) return czero<T>();
+    return inter[(static_cast<long long>(z0 + b) * a.ncols + c) * n + pos];
+  }, [&](int b, int pos, cx<T> v) {
+    const int e = yEnt[pos];
+    if (e >= 0 && b < zl) out[cBase[e] + b] = cvt<typename BT::value_type>(v);
+  });
 }
 
 // ---------------------------------------------------------------- x stage
+// Backward x stage with the line-fast engine: lane (line = row y, pos = x)
+// reads column x of the intermediate (consecutive lanes -> consecutive y),
+// zero for x without sticks; C2R completes the row by hermitian symmetry on
+// the fly. The result is written row-contiguous from LDS.
 template <class Eng, typename T, bool R2C>
 __global__ void __launch_bounds__(kMaxThreads)
     x_backward_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, void* __restrict__ space,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
+  const int n = eng.n();
   const int zl = blockIdx.y;
   const int y0 = blockIdx.x * B;
-  zero_lds(lds, eng.input_elems());
+  int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
   __syncthreads();
-  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.Y;
-  for (int idx = threadIdx.x; idx < a.ncols * B; idx += blockDim.x) {
-    const int c = idx / B, yy = idx - c * B;
-    if (y0 + yy < a.Y) lds[eng.in_at(yy, a.colX[c])] = src[static_cast<long long>(c) * a.Y + y0 + yy];
-  }
+  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
   __syncthreads();
-  if (R2C) {
-    const int ext = a.n - a.nFreq;
-    for (int idx = threadIdx.x; idx < B * ext; idx += blockDim.x) {
-      const int yy = idx / ext, x = a.nFreq + idx % ext;
-      lds[eng.in_at(yy, x)] = conj(lds[eng.in_at(yy, a.n - x)]);
+  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.Y + y0;
+  const int yl = min(B, a.Y - y0);
+  eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
+    if (b >= yl) return czero<T>();
+    if (R2C && pos >= a.nFreq) {
+      const int c = xCol[n - pos];
+      return c < 0 ? czero<T>() : conj(src[static_cast<long long>(c) * a.Y + b]);
     }
-    __syncthreads();
-  }
-  eng.lds_to_global(lds, tw, [&](int b, int pos, cx<T> v) {
-    const int y = y0 + b;
-    if (y < a.Y) {
-      const long long row = (static_cast<long long>(zl) * a.Y + y) * a.n;
-      if (R2C)
-        static_cast<T*>(space)[row + pos] = v.x;
-      else
-        static_cast<cx<T>*>(space)[row + pos] = v;
-    }
+    const int c = xCol[pos];
+    return c < 0 ? czero<T>() : src[static_cast<long long>(c) * a.Y + b];
   });
+  for (int idx = threadIdx.x; idx < yl * n; idx += blockDim.x) {
+    const int b = idx / n, pos = idx - b * n;
+    const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
+    if (R2C)
+      static_cast<T*>(space)[row + pos] = lds[eng.out_at(b, pos)].x;
+    else
+      static_cast<cx<T>*>(space)[row + pos] = lds[eng.out_at(b, pos)];
+  }
 }
 
+// Forward x stage, line-fast engine: lanes read row segments of the space
+// domain and write the columns that hold sticks straight into [z][column][y]
+// (consecutive lanes -> consecutive y); R2C reads real rows.
 template <class Eng, typename T, bool R2C>
 __global__ void __launch_bounds__(kMaxThreads)
     x_forward_kernel(Eng eng, XArgs a, const void* __restrict__ space, cx<T>* __restrict__ inter,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
+  const int n = eng.n();
   const int zl = blockIdx.y;
   const int y0 = blockIdx.x * B;
-  eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
-    const int y = y0 + b;
-    if (y >= a.Y) return czero<T>();
-    const long long row = (static_cast<long long>(zl) * a.Y + y) * a.n;
+  int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
+  __syncthreads();
+  const int yl = min(B, a.Y - y0);
+  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.Y + y0;
+  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+    if (b >= yl) return czero<T>();
+    const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
     if (R2C) return mk<T>(static_cast<const T*>(space)[row + pos], T(0));
     return static_cast<const cx<T>*>(space)[row + pos];
+  }, [&](int b, int pos, cx<T> v) {
+    const int c = xCol[pos];
+    if (c >= 0 && b < yl) dst[static_cast<long long>(c) * a.Y + b] = v;
   });
-  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.Y;
-  for (int idx = threadIdx.x; idx < a.ncols * B; idx += blockDim.x) {
-    const int c = idx / B, yy = idx - c * B;
-    if (y0 + yy < a.Y) dst[static_cast<long long>(c) * a.Y + y0 + yy] = lds[eng.out_at(yy, a.colX[c])];
-  }
 }
 
 // ------------------------------------------------------------ host helpers
@@ -294,12 +559,12 @@ inline void prepare_kernel(K kernel, std::size_t ldsBytes) {
 
 // Calls f(engine, threads, lines, ldsBytes) with the CT engine of length n if
 // there is one, else with the RT engine.
-template <typename T, int S, class F>
+template <typename T, int S, bool LF = false, class F>
 inline void with_engine(int n, F&& f) {
   switch (n) {
 #define SPFFT_CT_CASE(NN)                                                         \
   case NN: {                                                                      \
-    using E = CtEng<T, NN, S>;                                                    \
+    using E = CtEng<T, NN, S, LF>;                                                \
     f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                             \
     return;                                                                       \
   }

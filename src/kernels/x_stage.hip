@@ -8,10 +8,11 @@ template <typename T>
 void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space,
                        const cx<T>* tw, hipStream_t stream) {
   if (a.L <= 0 || a.Y <= 0) return;
-  with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
+  with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_backward_kernel<decltype(eng), T, true> : x_backward_kernel<decltype(eng), T, false>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), lds, stream, eng, a,
+    const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
+    prepare_kernel(k, ldsTotal);
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), ldsTotal, stream, eng, a,
                        inter, space, tw);
     gpu_check_launch("x_backward", stream);
   });
@@ -21,10 +22,11 @@ template <typename T>
 void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
                       const cx<T>* tw, hipStream_t stream) {
   if (a.L <= 0 || a.Y <= 0) return;
-  with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
+  with_engine<T, -1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_forward_kernel<decltype(eng), T, true> : x_forward_kernel<decltype(eng), T, false>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), lds, stream, eng, a,
+    const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
+    prepare_kernel(k, ldsTotal);
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), ldsTotal, stream, eng, a,
                        space, inter, tw);
     gpu_check_launch("x_forward", stream);
   });

@@ -11,8 +11,9 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
   if (a.numSticks <= 0) return;
   with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = z_backward_kernel<decltype(eng), T, BT>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), lds, stream, eng, a,
+    const std::size_t ldsTotal = lds + run_table_bytes(lines);
+    prepare_kernel(k, ldsTotal);
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        values, out, tw);
     gpu_check_launch("z_backward", stream);
   });
@@ -24,8 +25,9 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
   if (a.numSticks <= 0) return;
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = z_forward_kernel<decltype(eng), T, BT>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), lds, stream, eng, a,
+    const std::size_t ldsTotal = lds + run_table_bytes(lines);
+    prepare_kernel(k, ldsTotal);
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        in, values, scale, tw);
     gpu_check_launch("z_forward", stream);
   });

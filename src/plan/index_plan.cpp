@@ -203,6 +203,36 @@ IndexPlan::IndexPlan(Communicator* comm, SpfftTransformType t, int dX, int dY, i
   numLocalElements = numLocal;
   runs = std::move(conv.runs);
   stickRunOffsets = std::move(conv.runOffsets);
+  {
+    // stick descriptors (simple sticks: values contiguous, <= 2 z-runs)
+    const int S = static_cast<int>(stickRunOffsets.size()) - 1;
+    simpleSticks = true;
+    stickDescs.assign(std::max(0, S), StickDesc{});
+    for (int s = 0; s < S && simpleSticks; ++s) {
+      const int q0 = stickRunOffsets[s], q1 = stickRunOffsets[s + 1];
+      const int nr = q1 - q0;
+      StickDesc d{};
+      if (nr == 0 || nr > 2) {
+        simpleSticks = nr == 0;
+        stickDescs[s] = d;
+        continue;
+      }
+      const StickRun& a = runs[q0];
+      d.valueStart = a.valueStart;
+      d.count = a.length;
+      d.z0 = a.zStart;
+      d.len0 = a.length;
+      d.z1 = 0;
+      if (nr == 2) {
+        const StickRun& b = runs[q0 + 1];
+        if (b.valueStart != a.valueStart + a.length) simpleSticks = false;
+        d.count += b.length;
+        d.z1 = b.zStart;
+      }
+      stickDescs[s] = d;
+    }
+    if (!simpleSticks) stickDescs.clear();
+  }
   maxSticks = *std::max_element(sticksPerRank.begin(), sticksPerRank.end());
   maxPlanes = *std::max_element(planesPerRank.begin(), planesPerRank.end());
   for (int s : sticksPerRank) totalSticks += s;

@@ -28,6 +28,19 @@ struct StickRun {
   std::int32_t stick;       // local stick index
 };
 
+// Per-stick descriptor for the common case where a stick's values are
+// contiguous in value order and form at most two z-runs (e.g. a centred
+// sphere: z = 0..h then n-h..n-1). Lets the z-stage map (stick, j) -> (value,
+// z) with two compares instead of a run search.
+struct StickDesc {
+  std::int32_t valueStart;  // first value of the stick
+  std::int32_t count;       // number of values
+  std::int32_t z0;          // storage z of value j < len0 is z0 + j
+  std::int32_t len0;
+  std::int32_t z1;          // storage z of value j >= len0 is z1 + (j - len0)
+  std::int32_t pad[3];
+};
+
 class IndexPlan {
 public:
   // comm == nullptr (or size 1 and localZLength == dimZ) -> local plan.
@@ -53,6 +66,8 @@ public:
   std::vector<StickRun> runs;         // grouped by stick (stable in value order)
   std::vector<int> stickRunOffsets;   // local_sticks()+1
   int zeroStick = -1;                 // local index of the (0,0) stick, -1 if not local
+  std::vector<StickDesc> stickDescs;  // filled when every local stick is "simple"
+  bool simpleSticks = false;
 
   // x-columns over ALL ranks' sticks (the y-stage works on these)
   std::vector<int> colX;        // storage x of column c, ascending
