@@ -60,11 +60,14 @@ SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchan
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 
-/* Execute on `hipStream` (hipStream_t). synchronous = 0: return after enqueue. */
+/* Execute on `hipStream` (hipStream_t, NULL = legacy default stream).
+ * synchronous = 0: return after enqueue. reset_stream: back to the private stream. */
 SPFFT_EXPORT SpfftError spfft_amd_transform_set_stream(SpfftTransform transform, void* hipStream,
                                                        int synchronous);
 SPFFT_EXPORT SpfftError spfft_amd_float_transform_set_stream(SpfftFloatTransform transform,
                                                              void* hipStream, int synchronous);
+SPFFT_EXPORT SpfftError spfft_amd_transform_reset_stream(SpfftTransform transform);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_reset_stream(SpfftFloatTransform transform);
 SPFFT_EXPORT SpfftError spfft_amd_transform_synchronize(SpfftTransform transform);
 SPFFT_EXPORT SpfftError spfft_amd_float_transform_synchronize(SpfftFloatTransform transform);
 SPFFT_EXPORT SpfftError spfft_amd_transform_local_z_offset_rank(SpfftTransform transform, int rank,

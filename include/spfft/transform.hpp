@@ -67,9 +67,12 @@ public:
   void backward(const double* input, SpfftProcessingUnitType outputLocation);
 
   /* ---- SpFFT-AMD extensions ------------------------------------------------ */
-  /* Run GPU work on `hipStream` (a hipStream_t). With synchronous == false the
-   * calls return after enqueueing; call synchronize() before touching results. */
+  /* Run GPU work on `hipStream` (a hipStream_t; nullptr = legacy default stream).
+   * With synchronous == false the calls return after enqueueing; call
+   * synchronize() before touching results. */
   void set_execution_stream(void* hipStream, bool synchronous);
+  /* Back to the private stream (ordered after the legacy default stream, synchronous). */
+  void reset_execution_stream();
   void synchronize();
 
   /* Step-wise execution (forward = xy, exchange, z; backward = z, exchange, xy). */

@@ -165,7 +165,12 @@ class _GridBase:
             dim_z, local_z_length, n, int(index_format),
             idx.ctypes.data if n else None))
         cls = TransformFloat if self._single else Transform
-        return cls(h, self)
+        t = cls(h, self)
+        if ProcessingUnit(processing_unit) == ProcessingUnit.GPU and torch is not None:
+            # torch semantics: run on the current torch stream (ordered with torch work
+            # on it, no cross-stream event per call); calls stay synchronous.
+            t.set_stream(torch.cuda.current_stream(), synchronous=True)
+        return t
 
 
 class Grid(_GridBase):
@@ -188,6 +193,8 @@ class _TransformBase:
         self._grid = grid  # keeps the grid (buffers) alive
         self._prec = _Precision(self._single)
         self._stream = None
+        self._cache = {}
+        self._views = {}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -203,8 +210,13 @@ class _TransformBase:
         return self._h
 
     def _get(self, name, ll=False):
+        # every getter of a transform is immutable after creation: cache it
+        c = self._cache.get(name)
+        if c is not None:
+            return c
         v = ctypes.c_longlong() if ll else ctypes.c_int()
         _check(self._prec.fn("transform_" + name)(self._h, ctypes.byref(v)))
+        self._cache[name] = v.value
         return v.value
 
     type = property(lambda self: TransformType(self._get("type")))
@@ -228,7 +240,10 @@ class _TransformBase:
     def clone(self):
         h = ctypes.c_void_p()
         _check(self._prec.fn("transform_clone")(self._h, ctypes.byref(h)))
-        return type(self)(h, None)
+        t = type(self)(h, None)
+        if self._stream is not None:
+            t.set_stream(self._stream)
+        return t
 
     # ---------------------------------------------------------------- data
     def space_domain_shape(self):
@@ -242,7 +257,15 @@ class _TransformBase:
     def space_domain(self, location=ProcessingUnit.HOST):
         """View of the space-domain slab [local_z][y][x] (complex, or real for R2C).
 
-        HOST: numpy array; GPU: torch tensor on the grid's device (zero copy)."""
+        HOST: numpy array; GPU: torch tensor on the grid's device (zero copy).
+        The view is created once per location and reused (the slab never moves)."""
+        v = self._views.get(int(location))
+        if v is None:
+            v = self._make_view(location)
+            self._views[int(location)] = v
+        return v
+
+    def _make_view(self, location):
         shape = self.space_domain_shape()
         real = self.type == TransformType.R2C
         ptr = self.space_domain_ptr(location)
@@ -298,11 +321,17 @@ class _TransformBase:
 
     # --------------------------------------------------- streams / step API
     def set_stream(self, stream=None, synchronous: bool = True):
-        """Execute on a HIP stream (int handle or torch.cuda.Stream); None = own stream."""
-        if stream is not None and not isinstance(stream, int):
+        """Execute on a HIP stream (int handle or torch.cuda.Stream; 0 = legacy default
+        stream). None returns to the library's private stream."""
+        if stream is None:
+            self._stream = None
+            _check(self._prec.amd_fn("transform_reset_stream")(self._h))
+            return
+        if not isinstance(stream, int):
             stream = stream.cuda_stream
         self._stream = stream
-        _check(self._prec.amd_fn("transform_set_stream")(self._h, stream, 1 if synchronous else 0))
+        _check(self._prec.amd_fn("transform_set_stream")(self._h, stream or None,
+                                                        1 if synchronous else 0))
 
     def synchronize(self):
         _check(self._prec.amd_fn("transform_synchronize")(self._h))

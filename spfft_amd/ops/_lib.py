@@ -87,6 +87,8 @@ def _prototypes(lib):
     sig["spfft_amd_transform_set_stream"] = [V, V, I]
     sig["spfft_amd_float_transform_set_stream"] = [V, V, I]
     sig["spfft_amd_transform_synchronize"] = [V]
+    sig["spfft_amd_transform_reset_stream"] = [V]
+    sig["spfft_amd_float_transform_reset_stream"] = [V]
     sig["spfft_amd_float_transform_synchronize"] = [V]
     sig["spfft_amd_transform_local_z_offset_rank"] = [V, I, c_int_p, c_int_p]
     sig["spfft_amd_transform_space_domain_dlpack"] = [V, I, c_void_pp]

@@ -352,6 +352,12 @@ SpfftError spfft_amd_float_transform_set_stream(SpfftFloatTransform t, void* str
   return with_handle<TransformFloat>(
       t, [&](TransformFloat& x) { x.set_execution_stream(stream, synchronous != 0); });
 }
+SpfftError spfft_amd_transform_reset_stream(SpfftTransform t) {
+  return with_handle<Transform>(t, [&](Transform& x) { x.reset_execution_stream(); });
+}
+SpfftError spfft_amd_float_transform_reset_stream(SpfftFloatTransform t) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.reset_execution_stream(); });
+}
 SpfftError spfft_amd_transform_synchronize(SpfftTransform t) {
   return with_handle<Transform>(t, [&](Transform& x) { x.synchronize(); });
 }

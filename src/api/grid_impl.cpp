@@ -35,8 +35,9 @@ void GridImpl<T>::init(int maxDimX, int maxDimY, int maxDimZ, int maxSticks, int
   pu_ = pu;
   numThreads_ = resolve_threads(numThreads);
   // 64-bit sizes; the public API keeps int (reference quirk: int views, gpu_array_view.hpp:71)
-  planeElems_ = checked_mul(checked_mul(maxX_, maxY_), std::max(1, maxLocalZ_));
-  exchElems_ = std::max(planeElems_, checked_mul(maxZ_, maxSticks_));
+  // room for row / stick padding (kMaxPad elements per row or stick)
+  planeElems_ = checked_mul(checked_mul(maxX_, maxY_ + kMaxPad), std::max(1, maxLocalZ_));
+  exchElems_ = std::max(planeElems_, checked_mul(maxZ_ + kMaxPad, maxSticks_));
   if (pu_ & SPFFT_PU_GPU) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {

@@ -17,6 +17,9 @@ namespace spfft {
 class DeviceBuffer;   // gpu/device_buffer.hpp
 class DeviceComm;     // gpu/device_comm.hpp
 
+// Largest row/stick padding (elements) a transform may add to its buffers.
+constexpr int kMaxPad = 32;
+
 template <typename T>
 class GridImpl {
 public:

@@ -46,6 +46,7 @@ namespace spfft {
     transform_->set_stream(hipStream, synchronous);                                              \
   }                                                                                              \
   void TRANSFORM::synchronize() { transform_->synchronize(); }                                   \
+  void TRANSFORM::reset_execution_stream() { transform_->reset_stream(); }                       \
   std::shared_ptr<Communicator> TRANSFORM::spfft_communicator() const {                          \
     return transform_->grid()->communicator();                                                   \
   }                                                                                              \

@@ -154,6 +154,12 @@ void TransformImpl<T>::set_stream(void* stream, bool synchronous) {
   gpu_->set_stream(static_cast<hipStream_t>(stream), synchronous);
 }
 
+template <typename T>
+void TransformImpl<T>::reset_stream() {
+  if (!gpu_) throw InvalidParameterError();
+  gpu_->reset_stream();
+}
+
 template class TransformImpl<double>;
 template class TransformImpl<float>;
 

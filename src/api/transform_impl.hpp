@@ -32,6 +32,7 @@ public:
   void backward_xy(SpfftProcessingUnitType outputLocation);
   void synchronize();
   void set_stream(void* stream, bool synchronous);
+  void reset_stream();
 
   T* space_domain_data(SpfftProcessingUnitType location);
 

@@ -1,6 +1,8 @@
 #include "gpu/gpu_executor.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/timing.hpp"
@@ -9,6 +11,15 @@
 #include "spfft/exceptions.hpp"
 
 namespace spfft {
+
+namespace {
+int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* e = std::getenv(name);
+  if (!e || !*e) return dflt;
+  const int v = std::atoi(e);
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+}  // namespace
 
 template <typename T>
 template <typename U>
@@ -27,8 +38,11 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   DeviceGuard guard(deviceId_);
   const IndexPlan& p = *plan_;
   const bool distributed = p.size > 1;
-  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()));
+  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()),
+                                 env_int("SPFFT_PAD_STICK", 8, 0, kMaxPad));
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
+  interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
+  chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
@@ -87,13 +101,32 @@ GpuExecutor<T>::~GpuExecutor() {
 
 template <typename T>
 void GpuExecutor<T>::set_stream(hipStream_t stream, bool synchronous) {
-  stream_ = stream ? stream : ownStream_->get();
+  stream_ = stream;
+  ownStreamActive_ = false;
   synchronous_ = synchronous;
+}
+
+template <typename T>
+void GpuExecutor<T>::reset_stream() {
+  stream_ = ownStream_->get();
+  ownStreamActive_ = true;
+  synchronous_ = true;
 }
 
 template <typename T>
 void GpuExecutor<T>::synchronize() {
   DeviceGuard guard(deviceId_);
+  if (gpu_sync_spin()) {
+    // poll: wakes within ~1 us of completion instead of the blocking wait's
+    // interrupt latency; falls back to the blocking wait after ~20 ms
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(stream_);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) gpu_check(e, "hipStreamQuery");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+  }
   gpu_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
@@ -101,7 +134,7 @@ template <typename T>
 void GpuExecutor<T>::order_after_default_stream() {
   // errors left behind by earlier (user) GPU work (reference: execution_gpu.cpp:251-253)
   if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
-  if (stream_ == ownStream_->get()) {
+  if (ownStreamActive_) {
     // order after work already queued on the legacy default stream (reference: execution_gpu.cpp:258-259)
     event_->record(nullptr);
     event_->wait_on(stream_);
@@ -140,6 +173,7 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
   a.runOffsets = runOffsets_ ? runOffsets_->data<int>() : nullptr;
   a.desc = descs_ ? descs_->data<StickDesc>() : nullptr;
   a.single = p.size == 1 ? 1 : 0;
+  a.stickStride = layout_.stickStride[0];
   a.zRank = zRank_ ? zRank_->data<int>() : nullptr;
   a.segDispl = segDispl_ ? segDispl_->data<long long>() : nullptr;
   a.segStride = segStride_ ? segStride_->data<long long>() : nullptr;
@@ -153,8 +187,10 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   dev::YArgs a{};
   a.ncols = p.num_columns();
   a.L = p.local_planes();
+  a.zBegin = 0;
   a.n = p.dimY;
   a.colOfX0 = p.type == SPFFT_TRANS_R2C ? p.colOfX0 : -1;
+  a.interStride = interStride_;
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
@@ -166,10 +202,12 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   const IndexPlan& p = *plan_;
   dev::XArgs a{};
   a.L = p.local_planes();
+  a.zBegin = 0;
   a.Y = p.dimY;
   a.n = p.dimX;
   a.nFreq = p.dimXFreq;
   a.ncols = p.num_columns();
+  a.interStride = interStride_;
   a.colX = colX_ ? colX_->data<int>() : nullptr;
   return a;
 }
@@ -232,15 +270,24 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
-  const auto ya = yargs();
-  if (floatExchange_)
-    dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
-                                         twY_->data<cx<T>>(), stream_);
-  else
-    dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
-                                     twY_->data<cx<T>>(), stream_);
-  dev::launch_x_backward<T>(xargs(), plan_->type == SPFFT_TRANS_R2C, inter, space,
-                            twX_->data<cx<T>>(), stream_);
+  // plane chunks: the intermediate of a chunk is read back by the x stage while
+  // it is still resident in the last-level (Infinity) cache
+  const int L = plan_->local_planes();
+  const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
+  for (int zb = 0; zb < L; zb += chunk) {
+    auto ya = yargs();
+    auto xa = xargs();
+    ya.zBegin = xa.zBegin = zb;
+    ya.L = xa.L = std::min(L, zb + chunk);
+    if (floatExchange_)
+      dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
+                                           twY_->data<cx<T>>(), stream_);
+    else
+      dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
+                                       twY_->data<cx<T>>(), stream_);
+    dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space,
+                              twX_->data<cx<T>>(), stream_);
+  }
   if (outputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
                              hipMemcpyDeviceToHost, stream_),
@@ -264,15 +311,22 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
   }
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
-  dev::launch_x_forward<T>(xargs(), plan_->type == SPFFT_TRANS_R2C, space, inter,
-                           twX_->data<cx<T>>(), stream_);
-  const auto ya = yargs();
-  if (floatExchange_)
-    dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
-                                        twY_->data<cx<T>>(), stream_);
-  else
-    dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
-                                    stream_);
+  const int L = plan_->local_planes();
+  const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
+  for (int zb = 0; zb < L; zb += chunk) {
+    auto ya = yargs();
+    auto xa = xargs();
+    ya.zBegin = xa.zBegin = zb;
+    ya.L = xa.L = std::min(L, zb + chunk);
+    dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
+                             twX_->data<cx<T>>(), stream_);
+    if (floatExchange_)
+      dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+                                          twY_->data<cx<T>>(), stream_);
+    else
+      dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab),
+                                      twY_->data<cx<T>>(), stream_);
+  }
 }
 
 template <typename T>

@@ -31,7 +31,11 @@ public:
 
   void synchronize();
   bool synchronous() const { return synchronous_; }
+  // Execute on `stream` (nullptr = the legacy default stream); work is then
+  // ordered by the stream itself. reset_stream() returns to the private stream,
+  // which is ordered after the default stream with an event per call.
   void set_stream(hipStream_t stream, bool synchronous);
+  void reset_stream();
   hipStream_t stream() const { return stream_; }
   T* space_domain(SpfftProcessingUnitType location);
 
@@ -50,10 +54,13 @@ private:
   std::shared_ptr<const IndexPlan> plan_;
   ExchangeLayout layout_;
   bool floatExchange_ = false;
+  long long interStride_ = 0;  // row stride of [z][column][y]
+  int chunkPlanes_ = 0;        // y/x stages interleaved per chunk of planes (0 = off)
   int deviceId_ = 0;
 
   std::unique_ptr<GpuStream> ownStream_;
   hipStream_t stream_ = nullptr;
+  bool ownStreamActive_ = true;
   bool synchronous_ = true;
   std::unique_ptr<GpuEvent> event_;
 

@@ -40,6 +40,14 @@ bool gpu_sync_debug() {
   return on;
 }
 
+bool gpu_sync_spin() {
+  static const bool spin = [] {
+    const char* e = std::getenv("SPFFT_SYNC");
+    return !(e && std::string(e) == "block");
+  }();
+  return spin;
+}
+
 void gpu_check_launch(const char* kernel, hipStream_t stream) {
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) throw_gpu_error(err == hipErrorInvalidValue ? hipErrorLaunchFailure : err, kernel);

@@ -21,6 +21,9 @@ inline void gpu_check(hipError_t err, const char* what = "") {
 // Debug mode (SPFFT_GPU_SYNC_DEBUG=1): synchronise and check after every launch
 // (reference: src/gpu_util/gpu_runtime.hpp:58-72 does this in Debug builds).
 bool gpu_sync_debug();
+// Synchronous calls poll the stream instead of blocking (SPFFT_SYNC=spin, default)
+// or block in the runtime (SPFFT_SYNC=block).
+bool gpu_sync_spin();
 void gpu_check_launch(const char* kernel, hipStream_t stream);
 
 class DeviceGuard {

@@ -21,7 +21,14 @@ namespace spfft {
 namespace dev {
 
 constexpr int kMaxThreads = 256;
-constexpr int kLdsBudget = 64 * 1024;
+#ifndef SPFFT_LDS_BUDGET
+#define SPFFT_LDS_BUDGET (64 * 1024)
+#endif
+#ifndef SPFFT_LF_MAX_LINES
+#define SPFFT_LF_MAX_LINES 16
+#endif
+// LDS per workgroup for the FFT lines (tuning knob; see tools/gpu_variants.sh)
+constexpr int kLdsBudget = SPFFT_LDS_BUDGET;
 
 template <typename T>
 struct LdsGeom;
@@ -83,10 +90,20 @@ template <>
 struct CtShape<128> {
   static constexpr int E = 16, R0 = 16, R1 = 8, R2 = 1;
 };
+#ifndef SPFFT_CT256_E
+#define SPFFT_CT256_E 16
+#endif
+#if SPFFT_CT256_E == 8
+template <>
+struct CtShape<256> {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4;
+};
+#else
 template <>
 struct CtShape<256> {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 1;
 };
+#endif
 template <>
 struct CtShape<512> {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8;
@@ -101,7 +118,7 @@ struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 // largest power of two <= b, at most 16 (line-fast lane mapping)
 __host__ __device__ constexpr int lf_lines(int b) {
   int p = 1;
-  while (p * 2 <= b && p * 2 <= 16) p *= 2;
+  while (p * 2 <= b && p * 2 <= SPFFT_LF_MAX_LINES) p *= 2;
   return p;
 }
 

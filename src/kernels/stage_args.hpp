@@ -27,7 +27,8 @@ struct ZArgs {
   const StickRun* runs;
   const int* runOffsets;
   const StickDesc* desc;     // non-null when every stick is simple (fast path)
-  int single;                // 1: exchange side is the plain [S][n] array
+  int single;                // 1: exchange side is the plain [S][stickStride] array
+  long long stickStride;     // element stride between sticks when single
   const int* zRank;          // n entries: rank owning plane z
   const long long* segDispl; // per rank
   const long long* segStride;
@@ -36,20 +37,24 @@ struct ZArgs {
 
 struct YArgs {
   int ncols;
-  int L;  // local planes
+  int L;       // end of the plane range processed (exclusive; = local planes)
+  int zBegin;  // first plane of the range (plane chunking)
   int n;  // dimY
   int colOfX0;  // column needing the x=0 plane hermitian fill, -1 for none
+  long long interStride;  // row stride of the [z][column][y] intermediate (>= n)
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
 };
 
 struct XArgs {
-  int L;
+  int L;       // end of the plane range (exclusive)
+  int zBegin;  // first plane of the range
   int Y;
   int n;      // dimX
   int nFreq;  // dimX/2+1 for R2C, dimX for C2C
   int ncols;
+  long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
   const int* colX;
 };
 

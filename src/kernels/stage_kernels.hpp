@@ -131,7 +131,7 @@ __device__ __forceinline__ void zero_lds(cx<T>* lds, int count) {
 }
 
 __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
-  if (a.single) return static_cast<long long>(s) * a.n + pos;
+  if (a.single) return static_cast<long long>(s) * a.stickStride + pos;
   const int r = a.zRank[pos];
   return a.segDispl[r] + static_cast<long long>(s) * a.segStride[r] + (pos - a.segZOff[r]);
 }
@@ -278,23 +278,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   zero_lds(lds, eng.input_elems());
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
-  if (a.desc) {
-    // simple sticks: (line b, j) -> value desc.valueStart + j, z from the two runs
-    StickDesc* d = reinterpret_cast<StickDesc*>(tableBase);
-    const int nl = min(B, a.numSticks - s0);
-    for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
-    __syncthreads();
-    const int n = eng.n();
-    gather_to_lds(lds, nl * n, [&](int idx) {
-      const int b = idx / n, j = idx - b * n;
-      return j < d[b].count ? values[d[b].valueStart + j] : czero<T>();
-    }, [&](int idx) {
-      const int b = idx / n, j = idx - b * n;
-      const StickDesc& q = d[b];
-      if (j >= q.count) return -1;
-      return eng.in_at(b, j < q.len0 ? q.z0 + j : q.z1 + (j - q.len0));
-    });
-  } else if (load_run_table(a, s0, B, tableBase, tab)) {
+  if (load_run_table(a, s0, B, tableBase, tab)) {
     // decompress: flat over the block's values, kGatherUnroll loads in flight per lane
     if (tab.contiguous) {
       const cx<T>* src = values + tab.runs[0].valueStart;
@@ -349,21 +333,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   // compress (+ scaling)
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
-  if (a.desc) {
-    StickDesc* d = reinterpret_cast<StickDesc*>(tableBase);
-    const int nl = min(B, a.numSticks - s0);
-    for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
-    __syncthreads();
-    const int n = eng.n();
-    for (int idx = threadIdx.x; idx < nl * n; idx += blockDim.x) {
-      const int b = idx / n, j = idx - b * n;
-      const StickDesc& q = d[b];
-      if (j < q.count) {
-        const int z = j < q.len0 ? q.z0 + j : q.z1 + (j - q.len0);
-        values[q.valueStart + j] = spfft::scale(lds[eng.out_at(b, z)], scale);
-      }
-    }
-  } else if (load_run_table(a, s0, B, tableBase, tab)) {
+  if (load_run_table(a, s0, B, tableBase, tab)) {
     for (int idx = threadIdx.x; idx < tab.total; idx += blockDim.x) {
       const int q = find_run(tab, idx);
       const StickRun& r = tab.runs[q];
@@ -385,6 +355,75 @@ __global__ void __launch_bounds__(kMaxThreads)
   }
 }
 
+// z stage for "simple" sticks (values of a stick contiguous, <= 2 z-runs; the
+// common stick-major input): every lane maps its FFT positions z straight to
+// value offsets, so values are loaded into registers and written back with
+// coalesced accesses and no LDS staging or zero-fill.
+__device__ __forceinline__ int desc_offset(const StickDesc& q, int z) {
+  int j = z - q.z0;
+  if (j >= 0 && j < q.len0) return j;
+  j = z - q.z1;
+  if (j >= 0 && j < q.count - q.len0) return q.len0 + j;
+  return -1;
+}
+
+template <class Eng, typename T, typename BT>
+__global__ void __launch_bounds__(kMaxThreads)
+    z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
+                           BT* __restrict__ out, const cx<T>* __restrict__ tw) {
+  SPFFT_LDS_DECL(T);
+  const int B = eng.lines();
+  const int n = eng.n();
+  const int s0 = blockIdx.x * B;
+  const int nl = min(B, a.numSticks - s0);
+  StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
+  __syncthreads();
+  auto load = [&](int b, int z) -> cx<T> {
+    if (b >= nl) return czero<T>();
+    const StickDesc& q = d[b];
+    const int j = desc_offset(q, z);
+    return j < 0 ? czero<T>() : values[q.valueStart + j];
+  };
+  auto store = [&](int b, int pos, cx<T> v) {
+    if (b < nl) out[seg_index(a, s0 + b, pos)] = cvt<typename BT::value_type>(v);
+  };
+  if (a.zeroStick >= s0 && a.zeroStick < s0 + nl) {
+    // block holding the (0,0) stick of an R2C transform: stage for the hermitian fill
+    for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+      const int b = idx / n, z = idx - b * n;
+      lds[eng.in_at(b, z)] = load(b, z);
+    }
+    __syncthreads();
+    hermitian_lines(eng, lds, a.zeroStick - s0, 1, n);
+    eng.lds_to_global(lds, tw, store);
+  } else {
+    eng.global_to_global(lds, tw, load, store);
+  }
+}
+
+template <class Eng, typename T, typename BT>
+__global__ void __launch_bounds__(kMaxThreads)
+    z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
+                          T scale, const cx<T>* __restrict__ tw) {
+  SPFFT_LDS_DECL(T);
+  const int B = eng.lines();
+  const int s0 = blockIdx.x * B;
+  const int nl = min(B, a.numSticks - s0);
+  StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
+  __syncthreads();
+  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+    if (b >= nl) return czero<T>();
+    return cvt<T>(in[seg_index(a, s0 + b, pos)]);
+  }, [&](int b, int pos, cx<T> v) {
+    if (b >= nl) return;
+    const StickDesc& q = d[b];
+    const int j = desc_offset(q, pos);
+    if (j >= 0) values[q.valueStart + j] = spfft::scale(v, scale);
+  });
+}
+
 // ---------------------------------------------------------------- y stage
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
 // loads straight from the stick side — consecutive lanes read consecutive z
@@ -398,7 +437,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int B = eng.lines();
   const int n = eng.n();
   const int c = blockIdx.x;
-  const int z0 = blockIdx.y * B;
+  const int z0 = a.zBegin + blockIdx.y * B;
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
   long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
@@ -437,7 +476,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   // rows of [z][column][y] are contiguous: coalesced copy-out
   for (int idx = threadIdx.x; idx < zl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
-    inter[(static_cast<long long>(z0 + b) * a.ncols + c) * n + pos] = lds[eng.out_at(b, pos)];
+    inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos] = lds[eng.out_at(b, pos)];
   }
 }
 
@@ -452,7 +491,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int B = eng.lines();
   const int n = eng.n();
   const int c = blockIdx.x;
-  const int z0 = blockIdx.y * B;
+  const int z0 = a.zBegin + blockIdx.y * B;
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
   long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
@@ -467,7 +506,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int zl = min(B, a.L - z0);
   eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return inter[(static_cast<long long>(z0 + b) * a.ncols + c) * n + pos];
+    return inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos];
   }, [&](int b, int pos, cx<T> v) {
     const int e = yEnt[pos];
     if (e >= 0 && b < zl) out[cBase[e] + b] = cvt<typename BT::value_type>(v);
@@ -486,23 +525,23 @@ __global__ void __launch_bounds__(kMaxThreads)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int zl = blockIdx.y;
+  const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
   __syncthreads();
   for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
   __syncthreads();
-  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.Y + y0;
+  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   const int yl = min(B, a.Y - y0);
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xCol[n - pos];
-      return c < 0 ? czero<T>() : conj(src[static_cast<long long>(c) * a.Y + b]);
+      return c < 0 ? czero<T>() : conj(src[static_cast<long long>(c) * a.interStride + b]);
     }
     const int c = xCol[pos];
-    return c < 0 ? czero<T>() : src[static_cast<long long>(c) * a.Y + b];
+    return c < 0 ? czero<T>() : src[static_cast<long long>(c) * a.interStride + b];
   });
   for (int idx = threadIdx.x; idx < yl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
@@ -524,7 +563,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int zl = blockIdx.y;
+  const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
@@ -532,7 +571,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
   __syncthreads();
   const int yl = min(B, a.Y - y0);
-  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.Y + y0;
+  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
@@ -540,7 +579,7 @@ __global__ void __launch_bounds__(kMaxThreads)
     return static_cast<const cx<T>*>(space)[row + pos];
   }, [&](int b, int pos, cx<T> v) {
     const int c = xCol[pos];
-    if (c >= 0 && b < yl) dst[static_cast<long long>(c) * a.Y + b] = v;
+    if (c >= 0 && b < yl) dst[static_cast<long long>(c) * a.interStride + b] = v;
   });
 }
 

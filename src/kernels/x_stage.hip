@@ -7,12 +7,12 @@ namespace dev {
 template <typename T>
 void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space,
                        const cx<T>* tw, hipStream_t stream) {
-  if (a.L <= 0 || a.Y <= 0) return;
+  if (a.L <= a.zBegin || a.Y <= 0) return;
   with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_backward_kernel<decltype(eng), T, true> : x_backward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal, stream, eng, a,
                        inter, space, tw);
     gpu_check_launch("x_backward", stream);
   });
@@ -21,12 +21,12 @@ void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space
 template <typename T>
 void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
                       const cx<T>* tw, hipStream_t stream) {
-  if (a.L <= 0 || a.Y <= 0) return;
+  if (a.L <= a.zBegin || a.Y <= 0) return;
   with_engine<T, -1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_forward_kernel<decltype(eng), T, true> : x_forward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal, stream, eng, a,
                        space, inter, tw);
     gpu_check_launch("x_forward", stream);
   });

@@ -10,7 +10,8 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
                        hipStream_t stream) {
   if (a.numSticks <= 0) return;
   with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
-    auto k = z_backward_kernel<decltype(eng), T, BT>;
+    auto k = a.desc ? z_backward_desc_kernel<decltype(eng), T, BT>
+                    : z_backward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,
@@ -24,7 +25,8 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
                       hipStream_t stream) {
   if (a.numSticks <= 0) return;
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
-    auto k = z_forward_kernel<decltype(eng), T, BT>;
+    auto k = a.desc ? z_forward_desc_kernel<decltype(eng), T, BT>
+                    : z_forward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,

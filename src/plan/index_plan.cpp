@@ -272,7 +272,7 @@ IndexPlan::IndexPlan(Communicator* comm, SpfftTransformType t, int dX, int dY, i
   }
 }
 
-ExchangeLayout make_exchange_layout(const IndexPlan& p, bool buffered) {
+ExchangeLayout make_exchange_layout(const IndexPlan& p, bool buffered, int stickPad) {
   ExchangeLayout l;
   const int P = p.size;
   const i64 S = p.local_sticks();
@@ -285,11 +285,11 @@ ExchangeLayout make_exchange_layout(const IndexPlan& p, bool buffered) {
   l.slabCount.resize(P);
   if (P == 1) {
     l.stickDispl[0] = 0;
-    l.stickStride[0] = p.dimZ;
-    l.stickCount[0] = S * p.dimZ;
+    l.stickStride[0] = p.dimZ + stickPad;
+    l.stickCount[0] = S * (p.dimZ + stickPad);
     l.slabDispl[0] = 0;
-    l.slabStride = p.dimZ;
-    l.slabCount[0] = S * p.dimZ;
+    l.slabStride = p.dimZ + stickPad;
+    l.slabCount[0] = S * (p.dimZ + stickPad);
   } else if (l.buffered) {
     const i64 block = static_cast<i64>(p.maxSticks) * p.maxPlanes;
     for (int r = 0; r < P; ++r) {

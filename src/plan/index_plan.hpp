@@ -95,6 +95,8 @@ struct ExchangeLayout {
   std::vector<i64> colEntryBase;
 };
 
-ExchangeLayout make_exchange_layout(const IndexPlan& plan, bool buffered);
+// stickPad: extra elements between sticks of the single-rank layout (breaks the
+// power-of-two stride of [S][dimZ]; HBM channel spreading).
+ExchangeLayout make_exchange_layout(const IndexPlan& plan, bool buffered, int stickPad = 0);
 
 }  // namespace spfft
