@@ -40,13 +40,8 @@ def build(clean: bool = False, jobs: int | None = None, build_type: str = "Relea
     _run(["cmake", "--build", BUILD_DIR, "-j", str(jobs)], env=env)
     _check_targets()
     os.makedirs(NATIVE_DIR, exist_ok=True)
-    for so in glob.glob(os.path.join(BUILD_DIR, "libspfft_amd*.so*")):
-        if os.path.islink(so):
-            continue
-        base = os.path.basename(so)
-        # libspfft_amd.so.1.0.0 -> libspfft_amd.so (single file, no symlinks needed)
-        name = base.split(".so")[0] + ".so"
-        shutil.copy2(so, os.path.join(NATIVE_DIR, name))
+    for so in glob.glob(os.path.join(BUILD_DIR, "libspfft_amd*.so")):
+        shutil.copy2(so, os.path.join(NATIVE_DIR, os.path.basename(so)))
     for exe in ("spfft_bench", "spfft_native_tests", "spfft_mpi_tests", "example_c",
                 "example_cpp", "example_f90"):
         src = os.path.join(BUILD_DIR, exe)

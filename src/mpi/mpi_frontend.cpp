@@ -1,0 +1,251 @@
+// MPI front end (libspfft_amd_mpi): MPI_Comm-taking constructors and getters
+// of the C++ and C APIs, the Fortran communicator shims, and the MPI
+// implementation of spfft::Communicator (reference: src/mpi_util/*, the MPI
+// constructors in src/spfft/grid.cpp:40-45 and the *_fortran shims at
+// grid.cpp:119-133, 278-290, transform.cpp:386-397).
+//
+// MPI is the control plane and the host data plane (MPI_Alltoallv on host
+// buffers); GPU grids bootstrap RCCL through allgather() and move data over
+// xGMI, never through MPI.
+#include <mpi.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <memory>
+#include <numeric>
+#include <vector>
+
+#include "spfft/communicator.hpp"
+#include "spfft/exceptions.hpp"
+#include "spfft/grid.h"
+#include "spfft/grid.hpp"
+#include "spfft/grid_float.h"
+#include "spfft/grid_float.hpp"
+#include "spfft/transform.h"
+#include "spfft/transform.hpp"
+#include "spfft/transform_float.h"
+#include "spfft/transform_float.hpp"
+
+namespace spfft {
+namespace {
+
+inline void mpi_check(int status) {
+  if (status != MPI_SUCCESS) throw MPIError();
+}
+
+bool mpi_finalized() {
+  int f = 0;
+  MPI_Finalized(&f);
+  return f != 0;
+}
+
+}  // namespace
+
+class MpiCommunicator : public Communicator {
+public:
+  // Duplicates `comm` (private message space per grid, reference
+  // mpi_communicator_handle.hpp:48-66).
+  explicit MpiCommunicator(MPI_Comm comm) {
+    int init = 0;
+    MPI_Initialized(&init);
+    if (!init) throw MPISupportError();
+    mpi_check(MPI_Comm_dup(comm, &comm_));
+    mpi_check(MPI_Comm_rank(comm_, &rank_));
+    mpi_check(MPI_Comm_size(comm_, &size_));
+  }
+  ~MpiCommunicator() override {
+    if (comm_ != MPI_COMM_NULL && !mpi_finalized()) MPI_Comm_free(&comm_);
+  }
+
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  MPI_Comm get() const { return comm_; }
+
+  void allgather(const void* send, void* recv, std::size_t bytes) override {
+    if (bytes > static_cast<std::size_t>(INT_MAX)) throw OverflowError();
+    mpi_check(MPI_Allgather(send, static_cast<int>(bytes), MPI_BYTE, recv, static_cast<int>(bytes),
+                            MPI_BYTE, comm_));
+  }
+
+  void alltoallv(const void* send, const std::size_t* sc, const std::size_t* sd, void* recv,
+                 const std::size_t* rc, const std::size_t* rd) override {
+    // counts/displacements are bytes; use the largest element unit that divides
+    // all of them so that int counts reach far beyond 2 GiB
+    std::size_t g = 0;
+    for (int r = 0; r < size_; ++r) g = std::gcd(g, std::gcd(std::gcd(sc[r], sd[r]), std::gcd(rc[r], rd[r])));
+    std::size_t unit = 1;
+    for (std::size_t u : {std::size_t(16), std::size_t(8), std::size_t(4)}) {
+      if (g % u == 0) {
+        unit = u;
+        break;
+      }
+    }
+    MPI_Datatype type;
+    mpi_check(MPI_Type_contiguous(static_cast<int>(unit), MPI_BYTE, &type));
+    mpi_check(MPI_Type_commit(&type));
+    std::vector<int> isc(size_), isd(size_), irc(size_), ird(size_);
+    for (int r = 0; r < size_; ++r) {
+      const std::size_t v[4] = {sc[r] / unit, sd[r] / unit, rc[r] / unit, rd[r] / unit};
+      for (std::size_t x : v)
+        if (x > static_cast<std::size_t>(INT_MAX)) {
+          MPI_Type_free(&type);
+          throw OverflowError();
+        }
+      isc[r] = static_cast<int>(v[0]);
+      isd[r] = static_cast<int>(v[1]);
+      irc[r] = static_cast<int>(v[2]);
+      ird[r] = static_cast<int>(v[3]);
+    }
+    const int st = MPI_Alltoallv(send, isc.data(), isd.data(), type, recv, irc.data(), ird.data(),
+                                 type, comm_);
+    MPI_Type_free(&type);
+    mpi_check(st);
+  }
+
+  void barrier() override { mpi_check(MPI_Barrier(comm_)); }
+
+  std::shared_ptr<Communicator> duplicate() const override {
+    return std::make_shared<MpiCommunicator>(comm_);
+  }
+
+private:
+  MPI_Comm comm_ = MPI_COMM_NULL;
+  int rank_ = 0, size_ = 1;
+};
+
+namespace {
+MPI_Comm comm_of(const std::shared_ptr<Communicator>& c) {
+  auto* m = dynamic_cast<MpiCommunicator*>(c.get());
+  if (m) return m->get();
+  if (!c) return MPI_COMM_SELF;  // local grid
+  throw InvalidParameterError();  // distributed over a non-MPI communicator
+}
+}  // namespace
+
+// ---------------------------------------------------------------- C++ API
+Grid::Grid(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns, int maxLocalZLength,
+           SpfftProcessingUnitType processingUnit, int maxNumThreads, MPI_Comm comm,
+           SpfftExchangeType exchangeType)
+    : Grid(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength, processingUnit,
+           maxNumThreads, std::make_shared<MpiCommunicator>(comm), exchangeType) {}
+
+GridFloat::GridFloat(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+                     int maxLocalZLength, SpfftProcessingUnitType processingUnit,
+                     int maxNumThreads, MPI_Comm comm, SpfftExchangeType exchangeType)
+    : GridFloat(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength, processingUnit,
+                maxNumThreads, std::make_shared<MpiCommunicator>(comm), exchangeType) {}
+
+MPI_Comm Grid::communicator() const { return comm_of(spfft_communicator()); }
+MPI_Comm GridFloat::communicator() const { return comm_of(spfft_communicator()); }
+MPI_Comm Transform::communicator() const { return comm_of(spfft_communicator()); }
+MPI_Comm TransformFloat::communicator() const { return comm_of(spfft_communicator()); }
+
+}  // namespace spfft
+
+// ------------------------------------------------------------------ C API
+using namespace spfft;
+
+namespace {
+template <class F>
+SpfftError guarded(F&& f) {
+  try {
+    f();
+    return SPFFT_SUCCESS;
+  } catch (const GenericError& e) {
+    return e.error_code();
+  } catch (...) {
+    return SPFFT_UNKNOWN_ERROR;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+SpfftError spfft_grid_create_distributed(SpfftGrid* grid, int maxDimX, int maxDimY, int maxDimZ,
+                                         int maxNumLocalZColumns, int maxLocalZLength,
+                                         SpfftProcessingUnitType processingUnit, int maxNumThreads,
+                                         MPI_Comm comm, SpfftExchangeType exchangeType) {
+  if (!grid) return SPFFT_INVALID_PARAMETER_ERROR;
+  return guarded([&] {
+    *grid = new Grid(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength,
+                     processingUnit, maxNumThreads, comm, exchangeType);
+  });
+}
+
+SpfftError spfft_float_grid_create_distributed(SpfftFloatGrid* grid, int maxDimX, int maxDimY,
+                                               int maxDimZ, int maxNumLocalZColumns,
+                                               int maxLocalZLength,
+                                               SpfftProcessingUnitType processingUnit,
+                                               int maxNumThreads, MPI_Comm comm,
+                                               SpfftExchangeType exchangeType) {
+  if (!grid) return SPFFT_INVALID_PARAMETER_ERROR;
+  return guarded([&] {
+    *grid = new GridFloat(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength,
+                          processingUnit, maxNumThreads, comm, exchangeType);
+  });
+}
+
+SpfftError spfft_grid_communicator(SpfftGrid grid, MPI_Comm* comm) {
+  if (!grid) return SPFFT_INVALID_HANDLE_ERROR;
+  return guarded([&] { *comm = static_cast<Grid*>(grid)->communicator(); });
+}
+SpfftError spfft_float_grid_communicator(SpfftFloatGrid grid, MPI_Comm* comm) {
+  if (!grid) return SPFFT_INVALID_HANDLE_ERROR;
+  return guarded([&] { *comm = static_cast<GridFloat*>(grid)->communicator(); });
+}
+SpfftError spfft_transform_communicator(SpfftTransform t, MPI_Comm* comm) {
+  if (!t) return SPFFT_INVALID_HANDLE_ERROR;
+  return guarded([&] { *comm = static_cast<Transform*>(t)->communicator(); });
+}
+SpfftError spfft_float_transform_communicator(SpfftFloatTransform t, MPI_Comm* comm) {
+  if (!t) return SPFFT_INVALID_HANDLE_ERROR;
+  return guarded([&] { *comm = static_cast<TransformFloat*>(t)->communicator(); });
+}
+
+// Fortran shims: communicators as Fortran integers (MPI_Comm_f2c / c2f)
+SPFFT_EXPORT SpfftError spfft_grid_create_distributed_fortran(
+    SpfftGrid* grid, int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+    int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads, int commFortran,
+    SpfftExchangeType exchangeType) {
+  return spfft_grid_create_distributed(grid, maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns,
+                                       maxLocalZLength, processingUnit, maxNumThreads,
+                                       MPI_Comm_f2c(commFortran), exchangeType);
+}
+SPFFT_EXPORT SpfftError spfft_float_grid_create_distributed_fortran(
+    SpfftFloatGrid* grid, int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
+    int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads, int commFortran,
+    SpfftExchangeType exchangeType) {
+  return spfft_float_grid_create_distributed(grid, maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns,
+                                             maxLocalZLength, processingUnit, maxNumThreads,
+                                             MPI_Comm_f2c(commFortran), exchangeType);
+}
+SPFFT_EXPORT SpfftError spfft_grid_communicator_fortran(SpfftGrid grid, int* commFortran) {
+  MPI_Comm c;
+  const SpfftError e = spfft_grid_communicator(grid, &c);
+  if (e == SPFFT_SUCCESS) *commFortran = MPI_Comm_c2f(c);
+  return e;
+}
+SPFFT_EXPORT SpfftError spfft_float_grid_communicator_fortran(SpfftFloatGrid grid,
+                                                              int* commFortran) {
+  MPI_Comm c;
+  const SpfftError e = spfft_float_grid_communicator(grid, &c);
+  if (e == SPFFT_SUCCESS) *commFortran = MPI_Comm_c2f(c);
+  return e;
+}
+// (reference quirk fixed: the transform shim takes a transform handle)
+SPFFT_EXPORT SpfftError spfft_transform_communicator_fortran(SpfftTransform t, int* commFortran) {
+  MPI_Comm c;
+  const SpfftError e = spfft_transform_communicator(t, &c);
+  if (e == SPFFT_SUCCESS) *commFortran = MPI_Comm_c2f(c);
+  return e;
+}
+SPFFT_EXPORT SpfftError spfft_float_transform_communicator_fortran(SpfftFloatTransform t,
+                                                                   int* commFortran) {
+  MPI_Comm c;
+  const SpfftError e = spfft_float_transform_communicator(t, &c);
+  if (e == SPFFT_SUCCESS) *commFortran = MPI_Comm_c2f(c);
+  return e;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+"""Runs the native (C/C++/Fortran) test programs and examples built by
+spfft_amd.build: the C++ unit-test runner, the MPI test runner under
+mpiexec with 1-4 ranks (reference: tests/CMakeLists.txt runs run_mpi_tests
+with mpiexec -n 1..4), and the C, C++ and Fortran examples (reference:
+examples/example.{c,cpp,f90}).
+
+GPU sub-cases inside the native runners skip themselves when no device is
+visible, so these tests are CPU-runnable; the GPU variant re-runs them on the
+MI355X box.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(REPO, "spfft_amd", "_native")
+MPIEXEC = shutil.which("mpiexec") or "/opt/conda/bin/mpiexec"
+
+
+def _prog(name):
+    path = os.path.join(NATIVE, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not built")
+    return path
+
+
+def _run(cmd, timeout=600):
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "2")
+    r = subprocess.run(cmd, cwd=NATIVE, env=env, capture_output=True, text=True, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, f"{cmd} exited {r.returncode}:\n{out[-4000:]}"
+    return out
+
+
+def test_native_unit_tests():
+    out = _run([_prog("spfft_native_tests")])
+    assert " 0 failed" in out
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4])
+def test_mpi_tests(nranks):
+    prog = _prog("spfft_mpi_tests")
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = _run([MPIEXEC, "-n", str(nranks), prog])
+    assert " 0 failed" in out
+
+
+@pytest.mark.parametrize("name", ["example_c", "example_cpp", "example_f90"])
+def test_examples(name):
+    out = _run([_prog(name)])
+    assert out.strip()
+
+
+@pytest.mark.gpu
+def test_native_unit_tests_gpu(gpu):
+    out = _run([_prog("spfft_native_tests")])
+    assert " 0 failed" in out and "SKIP" not in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [1, 2])
+def test_mpi_tests_gpu(gpu, nranks):
+    prog = _prog("spfft_mpi_tests")
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = _run([MPIEXEC, "-n", str(nranks), prog])
+    assert " 0 failed" in out
