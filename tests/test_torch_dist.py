@@ -1,0 +1,48 @@
+"""Multi-process distributed transforms over torch.distributed (gloo control
+plane, one OS process per rank), the same launch path bench.py uses.
+
+CPU: host transforms, every exchange type, 2 and 3 ranks.
+GPU: 2 ranks sharing the box's single MI355X — exercises the library's RCCL
+communicator bootstrap (ncclUniqueId via allgather) and grouped send/recv.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROBE = os.path.join(REPO, "tools", "rccl_probe.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(nproc, *args, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", PROBE, *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert out.count(" OK") == nproc, out[-4000:]
+
+
+@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "COMPACT_BUFFERED_FLOAT", "BUFFERED",
+                                      "BUFFERED_FLOAT", "UNBUFFERED"])
+def test_torch_dist_host(exchange):
+    _launch(2, exchange, "--host")
+
+
+def test_torch_dist_host_3ranks():
+    _launch(3, "COMPACT_BUFFERED", "--host")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "BUFFERED_FLOAT"])
+def test_torch_dist_rccl(gpu, exchange):
+    _launch(2, exchange)
