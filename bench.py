@@ -57,12 +57,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one rank per GPU; more ranks than GPUs (rehearsal on a small box) share
+    # devices round-robin and the library then moves data by IPC peer writes
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # torch.distributed is the control plane only (plan setup, barriers,
+        # the timing reduction): gloo. The transform's all-to-all runs on the
+        # library's own RCCL communicator over xGMI.
+        dist.init_process_group("gloo")
 
     n = a.size
     dims = (n, n, n)
@@ -89,6 +95,7 @@ def main():
                                  transform_type=ttype, exchange_type=exch, single=single)
         grid, t, local, zlen = setup.grid, setup.transform, setup.indices, setup.z_length
 
+    plane = grid.data_plane if world > 1 else "none"
     if a.sync == "stream":
         t.set_stream(torch.cuda.current_stream(), synchronous=False)
 
@@ -121,7 +128,7 @@ def main():
     barrier()
     elapsed = t1 - t0
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ms_per_step = 1e3 * elapsed / a.steps
@@ -149,6 +156,7 @@ def main():
                 "parallelism": f"slab/pencil x{world} ({a.exchange} all-to-all)",
                 "num_frequency_values": int(len(gidx)),
                 "exchange": a.exchange,
+                "data_plane": plane,
                 "sync": a.sync,
                 "step": "1 backward + 1 forward transform",
             },

@@ -57,6 +57,11 @@ SPFFT_EXPORT SpfftError spfft_amd_float_grid_create_distributed(
     int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads,
     SpfftAmdComm comm, SpfftExchangeType exchangeType);
 SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchangeType* type);
+/* GPU data plane of a distributed grid: "rccl", "ipc" (peer writes across
+ * processes), "peer" (peer writes inside a local group), "loopback", or "none"
+ * (local or host-only grid). Collective on first call (creates the data plane). */
+SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name);
+SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 

@@ -148,6 +148,14 @@ class _GridBase:
         return ExchangeType(v.value)
 
     @property
+    def data_plane(self) -> str:
+        """GPU data plane of a distributed grid: "rccl", "ipc", "peer", "loopback" or
+        "none". Collective on first use (it creates the data plane)."""
+        v = ctypes.c_char_p()
+        _check(self._prec.amd_fn("grid_data_plane")(self._h, ctypes.byref(v)))
+        return v.value.decode()
+
+    @property
     def communicator(self):
         return self._comm
 
@@ -166,9 +174,13 @@ class _GridBase:
             idx.ctypes.data if n else None))
         cls = TransformFloat if self._single else Transform
         t = cls(h, self)
-        if ProcessingUnit(processing_unit) == ProcessingUnit.GPU and torch is not None:
+        in_process = getattr(self._comm, "in_process", False)
+        if ProcessingUnit(processing_unit) == ProcessingUnit.GPU and torch is not None \
+                and not in_process:
             # torch semantics: run on the current torch stream (ordered with torch work
             # on it, no cross-stream event per call); calls stay synchronous.
+            # Ranks of an in-process group keep private streams: they share torch's
+            # current stream, and one rank's exchange must not queue behind another's.
             t.set_stream(torch.cuda.current_stream(), synchronous=True)
         return t
 

@@ -17,6 +17,8 @@ def _check(code):
 class Communicator:
     """Owns a native SpfftAmdComm handle."""
 
+    in_process = False  # ranks are threads of this process (LocalGroup)
+
     def __init__(self, handle):
         self.handle = handle
 
@@ -49,6 +51,8 @@ class LocalGroup:
         arr = (ctypes.c_void_p * size)()
         _check(lib().spfft_amd_comm_create_local_group(size, arr))
         self.comms = [Communicator(ctypes.c_void_p(arr[r])) for r in range(size)]
+        for c in self.comms:
+            c.in_process = True
 
     def __getitem__(self, r):
         return self.comms[r]

@@ -7,7 +7,9 @@
 
 #include "api/transform_impl.hpp"
 #include "comm/callback_comm.hpp"
+#include "core/common.hpp"
 #include "core/timing.hpp"
+#include "gpu/device_comm.hpp"
 #include "spfft/amd.h"
 #include "spfft/exceptions.hpp"
 #include "spfft/grid.hpp"
@@ -34,12 +36,14 @@ thread_local std::string tlsLastError;
 
 template <class F>
 SpfftError guarded(F&& f) {
+  error_detail().clear();
   try {
     f();
     tlsLastError.clear();
     return SPFFT_SUCCESS;
   } catch (const GenericError& e) {
     tlsLastError = e.what();
+    if (!error_detail().empty()) tlsLastError += " [" + error_detail() + "]";
     return e.error_code();
   } catch (const std::exception& e) {
     tlsLastError = e.what();
@@ -129,6 +133,14 @@ void* export_space_domain(TR& t, SpfftProcessingUnitType loc) {
   return &h->managed;
 }
 
+}  // namespace
+
+namespace {
+template <class Impl>
+const char* data_plane_of(Impl& impl) {
+  if (!(impl.processing_unit() & SPFFT_PU_GPU) || impl.local()) return "none";
+  return impl.device_comm().kind();
+}
 }  // namespace
 
 extern "C" {
@@ -341,6 +353,15 @@ SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchangeType* type)
 }
 SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid, SpfftExchangeType* type) {
   return with_handle<GridFloat>(grid, [&](GridFloat& g) { *type = g.impl()->exchange_type(); });
+}
+
+SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name) {
+  if (!name) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<Grid>(grid, [&](Grid& g) { *name = data_plane_of(*g.impl()); });
+}
+SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name) {
+  if (!name) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<GridFloat>(grid, [&](GridFloat& g) { *name = data_plane_of(*g.impl()); });
 }
 
 SpfftError spfft_amd_transform_set_stream(SpfftTransform t, void* stream, int synchronous) {

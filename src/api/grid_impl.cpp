@@ -164,7 +164,11 @@ void* GridImpl<T>::device_slot(Slot s) {
 template <typename T>
 DeviceComm& GridImpl<T>::device_comm() {
   std::lock_guard<std::mutex> lock(allocMutex_);
-  if (!devComm_) devComm_ = DeviceComm::create(comm_, deviceId_);
+  if (!devComm_) {
+    void* const buffers[2] = {dev_[kStickSide] ? dev_[kStickSide]->data() : nullptr,
+                              dev_[kSlabSide] ? dev_[kSlabSide]->data() : nullptr};
+    devComm_ = DeviceComm::create(comm_, deviceId_, exchange_, buffers);
+  }
   return *devComm_;
 }
 

@@ -4,6 +4,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <limits>
+#include <string>
 
 #include "spfft/exceptions.hpp"
 #include "spfft/types.h"
@@ -11,6 +12,15 @@
 namespace spfft {
 
 using i64 = std::int64_t;
+
+// Detail text for the next error reported through the C API's
+// spfft_amd_last_error_message (the exception classes carry fixed texts, as in
+// the reference); consumed by the API guard of the same thread.
+inline std::string& error_detail() {
+  static thread_local std::string detail;
+  return detail;
+}
+inline void set_error_detail(std::string text) { error_detail() = std::move(text); }
 
 // Throws InvalidParameterError unless cond holds.
 inline void require_param(bool cond) {

@@ -1,24 +1,37 @@
 // GPU data plane for the pencil <-> slab redistribution.
 //  - RcclDeviceComm: RCCL grouped send/recv (all-to-all-v) enqueued on the
 //    execution stream; xGMI peer links carry every peer pair concurrently.
-//    Replaces MPI_Alltoall(v/w) on staged host buffers
+//    Replaces MPI_Alltoall(v) on staged host buffers
 //    (reference: src/transpose/transpose_mpi_compact_buffered_gpu.cpp:195-282).
-//  - LoopbackDeviceComm: in-process local group (several virtual ranks on
-//    one or more GPUs of one process) using device-to-device peer copies.
+//  - PeerDeviceComm: zero-copy peer writes. Every rank maps the exchange
+//    buffers of every other rank (IPC handles across processes, plain pointers
+//    inside a local group); the producing stage kernel (z-stage backward,
+//    y-stage forward) stores its output straight into the receiver's buffer
+//    over xGMI, framed by stream-ordered barrier kernels. This is the
+//    UNBUFFERED exchange (the reference's MPI_Alltoallw with derived datatypes,
+//    src/transpose/transpose_mpi_unbuffered_gpu.cpp:174-230, without any
+//    intermediate copy) and the data plane for ranks that share one GPU, where
+//    RCCL refuses to run.
+//  - LoopbackDeviceComm: in-process local group, device-to-device copies.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <memory>
 
 #include "spfft/communicator.hpp"
+#include "spfft/types.h"
 
 namespace spfft {
 
 class DeviceComm {
 public:
-  static std::unique_ptr<DeviceComm> create(const std::shared_ptr<Communicator>& comm, int device);
+  // Collective. `buffers` are the grid's two exchange slots (0 = stick side,
+  // 1 = slab side; base pointers of device allocations).
+  static std::unique_ptr<DeviceComm> create(const std::shared_ptr<Communicator>& comm, int device,
+                                            SpfftExchangeType exchange, void* const buffers[2]);
   virtual ~DeviceComm();
 
   // Byte counts / displacements, one entry per rank. Enqueued on `stream`;
@@ -29,6 +42,24 @@ public:
                          hipStream_t stream) = 0;
   // true if alltoallv() returns only after the data moved (host-synchronous).
   virtual bool host_synchronous() const = 0;
+
+  // Peer-write data plane: stage kernels store into peer_buffer(r, slot)
+  // directly. Every rank issues the same sequence of calls (transforms are
+  // collective), so the host-side bookkeeping below mirrors the peers' state:
+  //   prepare_write(slot): before remote stores into `slot` of the peers; a
+  //     barrier round is enqueued only if some rank may still read that slot
+  //     (a note_read(slot) since the last round);
+  //   complete_writes(): barrier round after the remote stores, before the
+  //     receivers read;
+  //   note_read(slot): a local kernel reading `slot` was enqueued.
+  virtual bool peer_writes() const { return false; }
+  virtual void* peer_buffer(int /*rank*/, int /*slot*/) const { return nullptr; }
+  virtual void prepare_write(int /*slot*/, hipStream_t /*stream*/) {}
+  virtual void complete_writes(hipStream_t /*stream*/) {}
+  virtual void note_read(int /*slot*/) {}
+  // Throws if an asynchronous failure (e.g. a barrier timeout) was recorded.
+  virtual void check() {}
+  virtual const char* kind() const = 0;
 };
 
 }  // namespace spfft

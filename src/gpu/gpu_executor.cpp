@@ -85,8 +85,49 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
       bwdRecvCounts_.push_back(layout_.slabCount[r] * eb);
       bwdRecvDispls_.push_back(layout_.slabDispl[r] * eb);
     }
-    grid_->device_comm();  // collective data-plane setup happens at plan time
+    // collective data-plane setup happens at plan time
+    peerWrites_ = grid_->device_comm().peer_writes();
+    if (peerWrites_) build_peer_tables();
   }
+}
+
+template <typename T>
+void GpuExecutor<T>::build_peer_tables() {
+  const IndexPlan& p = *plan_;
+  DeviceComm& dc = grid_->device_comm();
+  const int P = p.size, me = p.rank;
+  const i64 eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+  const char* stick = static_cast<const char*>(grid_->device_slot(GridImpl<T>::kStickSide));
+  const char* slab = static_cast<const char*>(grid_->device_slot(GridImpl<T>::kSlabSide));
+  auto elem_offset = [&](const void* peer, const char* local) -> long long {
+    if (!peer) throw InternalError();
+    const long long d = static_cast<const char*>(peer) - local;
+    if (d % eb != 0) throw InternalError();
+    return d / eb;
+  };
+  const i64 block = static_cast<i64>(p.maxSticks) * p.maxPlanes;
+  i64 sticksBefore = 0, planesBefore = 0;
+  for (int q = 0; q < me; ++q) {
+    sticksBefore += p.sticksPerRank[q];
+    planesBefore += p.planesPerRank[q];
+  }
+  // backward: my sticks' planes of rank r land in r's slab side, block "from me"
+  std::vector<long long> seg(P);
+  for (int r = 0; r < P; ++r) {
+    const i64 displ = layout_.buffered ? me * block : sticksBefore * p.planesPerRank[r];
+    seg[r] = elem_offset(dc.peer_buffer(r, GridImpl<T>::kSlabSide), stick) + displ;
+  }
+  upload(segDisplRemote_, seg);
+  // forward: column entries of rank r's sticks land in r's stick side, block "from me"
+  std::vector<long long> cb(p.colY.size());
+  std::vector<long long> base(P);
+  for (int r = 0; r < P; ++r) {
+    const i64 displ = layout_.buffered ? me * block : static_cast<i64>(p.sticksPerRank[r]) * planesBefore;
+    base[r] = elem_offset(dc.peer_buffer(r, GridImpl<T>::kStickSide), slab) + displ;
+  }
+  for (std::size_t k = 0; k < p.colY.size(); ++k)
+    cb[k] = base[p.colRank[k]] + static_cast<i64>(p.colLocal[k]) * layout_.slabStride;
+  upload(colBaseRemote_, cb);
 }
 
 template <typename T>
@@ -115,6 +156,13 @@ void GpuExecutor<T>::reset_stream() {
 
 template <typename T>
 void GpuExecutor<T>::synchronize() {
+  wait_stream();
+  // a peer barrier that timed out leaves a flag behind (data are incomplete)
+  if (peerWrites_) grid_->device_comm().check();
+}
+
+template <typename T>
+void GpuExecutor<T>::wait_stream() {
   DeviceGuard guard(deviceId_);
   if (gpu_sync_spin()) {
     // poll: wakes within ~1 us of completion instead of the blocking wait's
@@ -231,7 +279,13 @@ void GpuExecutor<T>::backward_z(const T* input) {
     }
   }
   void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
-  const auto a = zargs();
+  auto a = zargs();
+  if (peerWrites_) {
+    // the z stage stores straight into the peers' slab sides
+    grid_->device_comm().prepare_write(GridImpl<T>::kSlabSide, stream_);
+    a.segDispl = segDisplRemote_->data<long long>();
+    a.remote = 1;
+  }
   if (floatExchange_)
     dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
                                          twZ_->data<cx<T>>(), stream_);
@@ -258,6 +312,11 @@ void GpuExecutor<T>::exchange(bool backward) {
 template <typename T>
 void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_backward_exchange");
+  if (peerWrites_) {
+    DeviceGuard guard(deviceId_);
+    grid_->device_comm().complete_writes(stream_);
+    return;
+  }
   exchange(true);
 }
 
@@ -270,6 +329,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
+  if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
   // plane chunks: the intermediate of a chunk is read back by the x stage while
   // it is still resident in the last-level (Infinity) cache
   const int L = plan_->local_planes();
@@ -311,6 +371,8 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
   }
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
+  // the y stage stores straight into the peers' stick sides
+  if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
   const int L = plan_->local_planes();
   const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
   for (int zb = 0; zb < L; zb += chunk) {
@@ -318,6 +380,10 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     auto xa = xargs();
     ya.zBegin = xa.zBegin = zb;
     ya.L = xa.L = std::min(L, zb + chunk);
+    if (peerWrites_) {
+      ya.colBase = colBaseRemote_->data<long long>();
+      ya.remote = 1;
+    }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
                              twX_->data<cx<T>>(), stream_);
     if (floatExchange_)
@@ -332,6 +398,11 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
 template <typename T>
 void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_forward_exchange");
+  if (peerWrites_) {
+    DeviceGuard guard(deviceId_);
+    grid_->device_comm().complete_writes(stream_);
+    return;
+  }
   exchange(false);
 }
 
@@ -349,6 +420,7 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   if (p.numLocalElements > 0 && !output) throw InvalidParameterError();
   if (hostOut) values = staging(p.numLocalElements);
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kStickSide);
   const auto a = zargs();
   if (floatExchange_)
     dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,

@@ -44,6 +44,8 @@ private:
   U* upload(std::unique_ptr<DeviceBuffer>& buf, const std::vector<U>& v);
   void order_after_default_stream();
   void exchange(bool backward);
+  void build_peer_tables();
+  void wait_stream();
   dev::ZArgs zargs() const;
   dev::YArgs yargs() const;
   dev::XArgs xargs() const;
@@ -67,6 +69,11 @@ private:
   // device tables
   std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_, zRank_, segDispl_, segStride_, segZOff_;
   std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
+  // peer-write exchange (DeviceComm::peer_writes): the z stage (backward) and y
+  // stage (forward) store straight into the receivers' buffers; these tables
+  // hold those destinations as element offsets from the local buffer.
+  bool peerWrites_ = false;
+  std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
   std::unique_ptr<DeviceBuffer> twX_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;
   std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;

@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "core/common.hpp"
 #include "core/host_buffer.hpp"
 
 namespace spfft {
@@ -17,7 +18,9 @@ struct ExitHook {
 
 bool process_exiting() { return gExiting.load(); }
 
-void throw_gpu_error(hipError_t err, const char* /*what*/) {
+void throw_gpu_error(hipError_t err, const char* what) {
+  set_error_detail(std::string(what ? what : "") + ": " + hipGetErrorName(err) + " (" +
+                   hipGetErrorString(err) + ")");
   switch (err) {
     case hipErrorMemoryAllocation: throw GPUAllocationError();
     case hipErrorLaunchFailure:

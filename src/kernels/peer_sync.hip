@@ -1,0 +1,49 @@
+// Stream-ordered all-rank barrier for the peer-write (UNBUFFERED / IPC) data
+// plane. One 64-lane workgroup per call: lane q publishes this rank's epoch
+// into rank q's flag array (system-scope release store; the flag arrays are
+// uncached device memory mapped into every rank), then polls its own array
+// until every rank has reached the epoch. The poll is bounded: after
+// `timeoutTicks` wall-clock ticks the kernel records a failure in a
+// host-mapped word and exits, so a missing peer can never leave a wave
+// spinning on the GPU.
+#include <hip/hip_runtime.h>
+
+#include "kernels/peer_sync.hpp"
+#include "gpu/gpu_runtime.hpp"
+
+namespace spfft {
+namespace dev {
+
+__global__ void __launch_bounds__(64)
+    peer_barrier_kernel(unsigned long long* const* __restrict__ peerFlags,
+                        unsigned long long* myFlags, int me, int P, unsigned long long epoch,
+                        unsigned int* failure, long long timeoutTicks) {
+  // everything this rank's stream wrote before (local or remote) is visible
+  // system-wide before the epoch is published
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  for (int q = threadIdx.x; q < P; q += blockDim.x)
+    __hip_atomic_store(peerFlags[q] + me, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const long long t0 = wall_clock64();
+  for (int q = threadIdx.x; q < P; q += blockDim.x) {
+    while (__hip_atomic_load(myFlags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (wall_clock64() - t0 > timeoutTicks) {
+        __hip_atomic_fetch_or(failure, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+void launch_peer_barrier(unsigned long long* const* peerFlags, unsigned long long* myFlags, int me,
+                         int P, unsigned long long epoch, unsigned int* failure,
+                         long long timeoutTicks, hipStream_t stream) {
+  hipLaunchKernelGGL(peer_barrier_kernel, dim3(1), dim3(64), 0, stream, peerFlags, myFlags, me, P,
+                     epoch, failure, timeoutTicks);
+  gpu_check_launch("peer_barrier", stream);
+}
+
+}  // namespace dev
+}  // namespace spfft

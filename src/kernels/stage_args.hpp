@@ -33,6 +33,7 @@ struct ZArgs {
   const long long* segDispl; // per rank
   const long long* segStride;
   const int* segZOff;
+  int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
 };
 
 struct YArgs {
@@ -45,6 +46,7 @@ struct YArgs {
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
+  int remote;  // forward stores reach peers' memory: release system-wide at exit
 };
 
 struct XArgs {

@@ -130,6 +130,13 @@ __device__ __forceinline__ void zero_lds(cx<T>* lds, int count) {
   for (int i = threadIdx.x; i < count; i += blockDim.x) lds[i] = czero<T>();
 }
 
+// Peer-write exchange: this wave's stores to other GPUs' memory are written
+// back system-wide before the kernel ends (the barrier kernel that follows
+// publishes them to the receivers).
+__device__ __forceinline__ void release_remote(int remote) {
+  if (remote) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
 __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
   if (a.single) return static_cast<long long>(s) * a.stickStride + pos;
   const int r = a.zRank[pos];
@@ -316,6 +323,7 @@ __global__ void __launch_bounds__(kMaxThreads)
     const int s = s0 + b;
     if (s < a.numSticks) out[seg_index(a, s, pos)] = cvt<typename BT::value_type>(v);
   });
+  release_remote(a.remote);
 }
 
 template <class Eng, typename T, typename BT>
@@ -400,6 +408,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   } else {
     eng.global_to_global(lds, tw, load, store);
   }
+  release_remote(a.remote);
 }
 
 template <class Eng, typename T, typename BT>
@@ -511,6 +520,7 @@ __global__ void __launch_bounds__(kMaxThreads)
     const int e = yEnt[pos];
     if (e >= 0 && b < zl) out[cBase[e] + b] = cvt<typename BT::value_type>(v);
   });
+  release_remote(a.remote);
 }
 
 // ---------------------------------------------------------------- x stage

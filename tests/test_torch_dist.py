@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(nproc, *args, timeout=300):
+def _launch(nproc, *args, timeout=300, expect=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", PROBE, *args]
     env = dict(os.environ, OMP_NUM_THREADS="1")
@@ -30,6 +30,8 @@ def _launch(nproc, *args, timeout=300):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert out.count(" OK") == nproc, out[-4000:]
+    if expect:
+        assert out.count(f"[{expect}]") == nproc, out[-4000:]
 
 
 @pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "COMPACT_BUFFERED_FLOAT", "BUFFERED",
@@ -42,7 +44,18 @@ def test_torch_dist_host_3ranks():
     _launch(3, "COMPACT_BUFFERED", "--host")
 
 
+# Ranks sharing the box's single GPU: RCCL refuses duplicate devices, so the
+# library picks the IPC peer-write data plane (stage kernels store into the
+# other processes' exchange buffers; stream-ordered barrier kernels).
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "BUFFERED_FLOAT"])
-def test_torch_dist_rccl(gpu, exchange):
-    _launch(2, exchange)
+@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "BUFFERED_FLOAT", "UNBUFFERED",
+                                      "COMPACT_BUFFERED_FLOAT", "BUFFERED"])
+def test_torch_dist_ipc_shared_gpu(gpu, exchange):
+    _launch(2, exchange, "--iters=4", expect="ipc")
+
+
+@pytest.mark.gpu
+def test_torch_dist_ipc_3ranks_repeated(gpu):
+    # many back-to-back transforms with fresh data: a stale read of an earlier
+    # exchange (missing barrier / visibility) shows as a mismatch
+    _launch(3, "UNBUFFERED", "--iters=12", "--dims=64,60,48", expect="ipc")

@@ -38,23 +38,32 @@ def main():
     rank, P = dist.get_rank(), dist.get_world_size()
     comm = TorchDistComm()
     dims = (40, 36, 30)
+    iters = 3
+    for a in sys.argv[1:]:
+        if a.startswith("--iters="):
+            iters = int(a.split("=")[1])
+        if a.startswith("--dims="):
+            dims = tuple(int(v) for v in a.split("=")[1].split(","))
     gidx = sphere_indices(*dims, 0.5)
-    rng = np.random.default_rng(5)
-    vals = rng.standard_normal(len(gidx)) + 1j * rng.standard_normal(len(gidx))
-    ref = dense_backward(gidx, vals, dims)
     parts = distribute_sticks(gidx, P, dims)
-    s = make_distributed(comm, dims, gidx, processing_unit=pu,
-                         exchange_type=exchange)
+    s = make_distributed(comm, dims, gidx, processing_unit=pu, exchange_type=exchange)
     start = sum(len(p) for p in parts[:rank])
-    mine = vals[start:start + len(s.indices)]
-    v = mine if host else torch.as_tensor(mine, device=dev)
-    out = _np(s.transform.backward(v))
-    e1 = max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length])
-    f = _np(s.transform.forward(None, scaling=sp.Scaling.FULL))
-    e2 = max_rel_error(f, mine)
+    e1 = e2 = 0.0
+    # fresh values every iteration: a stale read of a previous exchange shows up
+    for it in range(iters):
+        rng = np.random.default_rng(5 + it)
+        vals = rng.standard_normal(len(gidx)) + 1j * rng.standard_normal(len(gidx))
+        ref = dense_backward(gidx, vals, dims)
+        mine = vals[start:start + len(s.indices)]
+        v = mine if host else torch.as_tensor(mine, device=dev)
+        out = _np(s.transform.backward(v))
+        e1 = max(e1, max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length]))
+        f = _np(s.transform.forward(None, scaling=sp.Scaling.FULL))
+        e2 = max(e2, max_rel_error(f, mine))
     tol = 1e-5 if "FLOAT" in exch_name else 1e-11
     ok = e1 < tol and e2 < tol
-    print(f"rank {rank}/{P} {exch_name}: backward err {e1:.2e} forward err {e2:.2e} "
+    kind = "" if host else f" [{s.grid.data_plane}]"
+    print(f"rank {rank}/{P} {exch_name}{kind} x{iters}: backward err {e1:.2e} forward err {e2:.2e} "
           f"{'OK' if ok else 'FAIL'}", flush=True)
     del s
     dist.barrier()
