@@ -37,11 +37,42 @@ def parse():
     ap.add_argument("--precision", default="double", choices=["double", "single"])
     ap.add_argument("--type", default="c2c", choices=["c2c", "r2c"])
     ap.add_argument("--timing", action="store_true", help="print the native timing tree")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing: round-trip error on every rank and, on one rank, the "
+                         "backward transform against the dense numpy oracle")
     ap.add_argument("--sync", default="stream", choices=["stream", "call"],
                     help="stream: transforms are stream-ordered on torch's current stream (no host "
                          "wait per call; the timed loop still ends with a device synchronize); "
                          "call: every backward/forward call blocks until done (SpFFT default)")
     return ap.parse_args()
+
+
+def _check(a, sp, t, values, gidx, dims, ttype, world):
+    """Max relative error of the round trip (and of the backward vs numpy on 1 rank)."""
+    import numpy as np
+    import torch
+    from spfft_amd.utils.oracle import dense_backward, max_rel_error
+    out = torch.empty_like(values)
+    space = t.backward(values)
+    torch.cuda.synchronize()
+    err = {}
+    if world == 1:
+        ref = dense_backward(gidx, values.cpu().numpy(), dims,
+                             r2c=(ttype == sp.TransformType.R2C))
+        err["backward_vs_numpy"] = max_rel_error(space.cpu().numpy(), ref)
+    t.forward(None, output=out, scaling=sp.Scaling.FULL)
+    torch.cuda.synchronize()
+    if ttype == sp.TransformType.R2C:
+        # random R2C input is not hermitian on the x = 0 plane: compare the second
+        # round trip with the first (the round trip is a projection)
+        ref_rt = out.clone()
+        t.backward(ref_rt)
+        t.forward(None, output=out, scaling=sp.Scaling.FULL)
+        torch.cuda.synchronize()
+        err["roundtrip"] = max_rel_error(out.cpu().numpy(), ref_rt.cpu().numpy())
+    else:
+        err["roundtrip"] = max_rel_error(out.cpu().numpy(), values.cpu().numpy())
+    return err
 
 
 def main():
@@ -131,6 +162,9 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    check = None
+    if a.check:
+        check = _check(a, sp, t, values, gidx, dims, ttype, world)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * a.steps / elapsed
     if rank == 0:
@@ -158,6 +192,7 @@ def main():
                 "exchange": a.exchange,
                 "data_plane": plane,
                 "sync": a.sync,
+                "check_error": check,
                 "step": "1 backward + 1 forward transform",
             },
         }

@@ -122,6 +122,27 @@ __host__ __device__ constexpr int lf_lines(int b) {
   return p;
 }
 
+#ifndef SPFFT_PROBE_NO_COMPUTE
+#define SPFFT_PROBE_NO_COMPUTE 0
+#endif
+#ifndef SPFFT_PROBE_NO_EXCHANGE
+#define SPFFT_PROBE_NO_EXCHANGE 0
+#endif
+#ifndef SPFFT_LF_STRIDE
+#define SPFFT_LF_STRIDE 1
+#endif
+// Line stride of the line-fast mapping: a 16-lane LDS access group (64 banks x
+// 4 B = 16 slots of 16 B for fp64, 32 slots of 8 B for fp32) holds lines
+// b = 0..B-1 at kMod/B consecutive lane positions t; with the stride
+// == kMod/B (mod kMod) line b, position t lands on slot b*kMod/B + t: distinct.
+template <typename T>
+__host__ __device__ constexpr int lf_padded_stride(int n, int b) {
+  int ls = n + ((n - 1) >> LdsGeom<T>::kShift) + 1;
+  const int want = b >= LdsGeom<T>::kMod ? 1 : (LdsGeom<T>::kMod / b) % LdsGeom<T>::kMod;
+  while (ls % LdsGeom<T>::kMod != want) ++ls;
+  return ls;
+}
+
 // LF (line-fast) selects the lane -> (line b, lane t) mapping:
 //  false: t fastest (a line's TP lanes adjacent; row-contiguous global access),
 //  true:  b fastest (B lines adjacent; column-contiguous global access, e.g. a
@@ -131,9 +152,10 @@ struct FftCT {
   using Sh = CtShape<N>;
   static constexpr int E = Sh::E;
   static constexpr int TP = N / E;  // lanes per line
-  static constexpr int LS = padded_stride<T>(N);
-  static constexpr int B0 = lines_per_block(TP, LS * static_cast<int>(sizeof(cx<T>)));
+  static constexpr int LS0 = padded_stride<T>(N);
+  static constexpr int B0 = lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)));
   static constexpr int B = LF ? lf_lines(B0) : B0;
+  static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B) : LS0;
   static constexpr int NT = B * TP;
   static constexpr int RL = Sh::R2 > 1 ? Sh::R2 : (Sh::R1 > 1 ? Sh::R1 : Sh::R0);
 
@@ -147,6 +169,9 @@ struct FftCT {
   // holds element j + r*N/R with j = t + k*TP)
   template <int R, int NS>
   __device__ static void compute(cx<T> (&v)[E], int t, const cx<T>* __restrict__ tw) {
+#if SPFFT_PROBE_NO_COMPUTE
+    return;  // timing probe only: results are wrong
+#endif
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {
       if (NS > 1) {
@@ -162,6 +187,9 @@ struct FftCT {
   // write pass outputs (Stockham positions) to LDS and read the next pass inputs
   template <int R, int NS, int RN>
   __device__ static void exchange(cx<T> (&v)[E], cx<T>* line, int t) {
+#if SPFFT_PROBE_NO_EXCHANGE
+    return;  // timing probe only: results are wrong
+#endif
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {

@@ -13,6 +13,80 @@
 namespace spfft {
 namespace dev {
 
+#ifndef SPFFT_XB_DIRECT
+#define SPFFT_XB_DIRECT 0
+#endif
+#ifndef SPFFT_YB_DIRECT
+#define SPFFT_YB_DIRECT 0
+#endif
+
+#ifndef SPFFT_NT
+#define SPFFT_NT 1
+#endif
+#ifndef SPFFT_NT_VALUES
+#define SPFFT_NT_VALUES 0
+#endif
+
+// Streaming global accesses: every stage reads and writes each element once, so
+// loads and stores carry the non-temporal hint (measured on MI355X: 268 MB copy
+// 6.15-6.28 TB/s with nt vs 5.65-5.88 TB/s without, tools/probes/hbm_copy.hip).
+template <typename T>
+__device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
+#if SPFFT_NT
+  using V = T __attribute__((ext_vector_type(2)));
+  const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+  return mk<T>(v.x, v.y);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
+#if SPFFT_NT
+  using V = T __attribute__((ext_vector_type(2)));
+  V w;
+  w.x = v.x;
+  w.y = v.y;
+  __builtin_nontemporal_store(w, reinterpret_cast<V*>(p));
+#else
+  *p = v;
+#endif
+}
+// Sparse frequency values: a stick's values rarely start on a cache-line
+// boundary, so neighbouring workgroups share lines; plain accesses keep them.
+template <typename T>
+__device__ __forceinline__ cx<T> ld_values(const cx<T>* p) {
+#if SPFFT_NT_VALUES
+  return ld_stream(p);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_values(cx<T>* p, cx<T> v) {
+#if SPFFT_NT_VALUES
+  st_stream(p, v);
+#else
+  *p = v;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ T ld_stream_real(const T* p) {
+#if SPFFT_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_stream_real(T* p, T v) {
+#if SPFFT_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // ------------------------------------------------------------ engine adapters
 template <typename T, int N, int S, bool LF = false>
 struct CtEng {
@@ -296,7 +370,7 @@ __global__ void __launch_bounds__(kMaxThreads)
     } else {
       gather_to_lds(lds, tab.total, [&](int idx) {
         const int q = find_run(tab, idx);
-        return values[tab.runs[q].valueStart + idx - tab.start[q]];
+        return ld_values(&values[tab.runs[q].valueStart + idx - tab.start[q]]);
       }, [&](int idx) {
         const int q = find_run(tab, idx);
         return eng.in_at(tab.runs[q].stick - s0, tab.runs[q].zStart + idx - tab.start[q]);
@@ -313,7 +387,7 @@ __global__ void __launch_bounds__(kMaxThreads)
       for (int q = a.runOffsets[s]; q < q1; ++q) {
         const StickRun r = a.runs[q];
         for (int j = lane; j < r.length; j += 64)
-          lds[eng.in_at(b, r.zStart + j)] = values[r.valueStart + j];
+          lds[eng.in_at(b, r.zStart + j)] = ld_values(&values[r.valueStart + j]);
       }
     }
   }
@@ -321,7 +395,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   if (a.zeroStick >= s0 && a.zeroStick < s0 + B) hermitian_lines(eng, lds, a.zeroStick - s0, 1, a.n);
   eng.lds_to_global(lds, tw, [&](int b, int pos, cx<T> v) {
     const int s = s0 + b;
-    if (s < a.numSticks) out[seg_index(a, s, pos)] = cvt<typename BT::value_type>(v);
+    if (s < a.numSticks) st_stream(&out[seg_index(a, s, pos)], cvt<typename BT::value_type>(v));
   });
   release_remote(a.remote);
 }
@@ -336,7 +410,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
-    return cvt<T>(in[seg_index(a, s, pos)]);
+    return cvt<T>(ld_stream(&in[seg_index(a, s, pos)]));
   });
   // compress (+ scaling)
   RunTable tab;
@@ -346,7 +420,7 @@ __global__ void __launch_bounds__(kMaxThreads)
       const int q = find_run(tab, idx);
       const StickRun& r = tab.runs[q];
       const int off = idx - tab.start[q];
-      values[r.valueStart + off] = spfft::scale(lds[eng.out_at(r.stick - s0, r.zStart + off)], scale);
+      st_values(&values[r.valueStart + off], spfft::scale(lds[eng.out_at(r.stick - s0, r.zStart + off)], scale));
     }
   } else {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -357,7 +431,7 @@ __global__ void __launch_bounds__(kMaxThreads)
       for (int q = a.runOffsets[s]; q < q1; ++q) {
         const StickRun r = a.runs[q];
         for (int j = lane; j < r.length; j += 64)
-          values[r.valueStart + j] = spfft::scale(lds[eng.out_at(b, r.zStart + j)], scale);
+          st_values(&values[r.valueStart + j], spfft::scale(lds[eng.out_at(b, r.zStart + j)], scale));
       }
     }
   }
@@ -391,10 +465,10 @@ __global__ void __launch_bounds__(kMaxThreads)
     if (b >= nl) return czero<T>();
     const StickDesc& q = d[b];
     const int j = desc_offset(q, z);
-    return j < 0 ? czero<T>() : values[q.valueStart + j];
+    return j < 0 ? czero<T>() : ld_values(&values[q.valueStart + j]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
-    if (b < nl) out[seg_index(a, s0 + b, pos)] = cvt<typename BT::value_type>(v);
+    if (b < nl) st_stream(&out[seg_index(a, s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
   if (a.zeroStick >= s0 && a.zeroStick < s0 + nl) {
     // block holding the (0,0) stick of an R2C transform: stage for the hermitian fill
@@ -424,12 +498,12 @@ __global__ void __launch_bounds__(kMaxThreads)
   __syncthreads();
   eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= nl) return czero<T>();
-    return cvt<T>(in[seg_index(a, s0 + b, pos)]);
+    return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
   }, [&](int b, int pos, cx<T> v) {
     if (b >= nl) return;
     const StickDesc& q = d[b];
     const int j = desc_offset(q, pos);
-    if (j >= 0) values[q.valueStart + j] = spfft::scale(v, scale);
+    if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
   });
 }
 
@@ -463,17 +537,28 @@ __global__ void __launch_bounds__(kMaxThreads)
   __syncthreads();
   const int zl = min(B, a.L - z0);
   if (c != a.colOfX0) {
+#if SPFFT_YB_DIRECT
+    eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+      const int e = yEnt[pos];
+      if (e < 0 || b >= zl) return czero<T>();
+      return cvt<T>(ld_stream(&in[cBase[e] + b]));
+    }, [&](int b, int pos, cx<T> v) {
+      if (b < zl) st_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], v);
+    });
+    return;
+#else
     eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
       const int e = yEnt[pos];
       if (e < 0 || b >= zl) return czero<T>();
-      return cvt<T>(in[cBase[e] + b]);
+      return cvt<T>(ld_stream(&in[cBase[e] + b]));
     });
+#endif
   } else {
     zero_lds(lds, eng.input_elems());
     __syncthreads();
     gather_to_lds(lds, ne * zl, [&](int idx) {
       const int e = idx / zl, zz = idx - e * zl;
-      return cvt<T>(in[cBase[e] + zz]);
+      return cvt<T>(ld_stream(&in[cBase[e] + zz]));
     }, [&](int idx) {
       const int e = idx / zl, zz = idx - e * zl;
       return eng.in_at(zz, cY[e]);
@@ -485,7 +570,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   // rows of [z][column][y] are contiguous: coalesced copy-out
   for (int idx = threadIdx.x; idx < zl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
-    inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos] = lds[eng.out_at(b, pos)];
+    st_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], lds[eng.out_at(b, pos)]);
   }
 }
 
@@ -515,10 +600,10 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int zl = min(B, a.L - z0);
   eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos];
+    return ld_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
   }, [&](int b, int pos, cx<T> v) {
     const int e = yEnt[pos];
-    if (e >= 0 && b < zl) out[cBase[e] + b] = cvt<typename BT::value_type>(v);
+    if (e >= 0 && b < zl) st_stream(&out[cBase[e] + b], cvt<typename BT::value_type>(v));
   });
   release_remote(a.remote);
 }
@@ -544,23 +629,35 @@ __global__ void __launch_bounds__(kMaxThreads)
   __syncthreads();
   const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   const int yl = min(B, a.Y - y0);
-  eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
+  auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xCol[n - pos];
-      return c < 0 ? czero<T>() : conj(src[static_cast<long long>(c) * a.interStride + b]);
+      return c < 0 ? czero<T>() : conj(ld_stream(&src[static_cast<long long>(c) * a.interStride + b]));
     }
     const int c = xCol[pos];
-    return c < 0 ? czero<T>() : src[static_cast<long long>(c) * a.interStride + b];
+    return c < 0 ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+  };
+  const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
+#if SPFFT_XB_DIRECT
+  // line-fast lanes store rows directly: a wave writes B rows x (64/B) consecutive x
+  eng.global_to_global(lds, tw, load, [&](int b, int pos, cx<T> v) {
+    if (b >= yl) return;
+    if (R2C)
+      st_stream_real(&static_cast<T*>(space)[row0 + static_cast<long long>(b) * n + pos], v.x);
+    else
+      st_stream(&static_cast<cx<T>*>(space)[row0 + static_cast<long long>(b) * n + pos], v);
   });
+#else
+  eng.global_to_lds(lds, tw, load);
   for (int idx = threadIdx.x; idx < yl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
-    const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
     if (R2C)
-      static_cast<T*>(space)[row + pos] = lds[eng.out_at(b, pos)].x;
+      st_stream_real(&static_cast<T*>(space)[row0 + idx], lds[eng.out_at(b, pos)].x);
     else
-      static_cast<cx<T>*>(space)[row + pos] = lds[eng.out_at(b, pos)];
+      st_stream(&static_cast<cx<T>*>(space)[row0 + idx], lds[eng.out_at(b, pos)]);
   }
+#endif
 }
 
 // Forward x stage, line-fast engine: lanes read row segments of the space
@@ -585,11 +682,11 @@ __global__ void __launch_bounds__(kMaxThreads)
   eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
-    if (R2C) return mk<T>(static_cast<const T*>(space)[row + pos], T(0));
-    return static_cast<const cx<T>*>(space)[row + pos];
+    if (R2C) return mk<T>(ld_stream_real(&static_cast<const T*>(space)[row + pos]), T(0));
+    return ld_stream(&static_cast<const cx<T>*>(space)[row + pos]);
   }, [&](int b, int pos, cx<T> v) {
     const int c = xCol[pos];
-    if (c >= 0 && b < yl) dst[static_cast<long long>(c) * a.interStride + b] = v;
+    if (c >= 0 && b < yl) st_stream(&dst[static_cast<long long>(c) * a.interStride + b], v);
   });
 }
 
