@@ -69,3 +69,33 @@ def test_mpi_tests_gpu(gpu, nranks):
         pytest.skip("mpiexec not available")
     out = _run([MPIEXEC, "-n", str(nranks), prog])
     assert " 0 failed" in out
+
+
+def test_bench_cli_host(tmp_path):
+    """C++ benchmark CLI (reference flags -d -r -o -m -s -t -e -p) on the host engine."""
+    import json
+    out = tmp_path / "b.json"
+    _run([_prog("spfft_bench"), "-d", "24", "20", "18", "-r", "2", "-o", str(out), "-e", "all",
+          "-p", "cpu", "--cutoff", "0.5", "-m", "2"])
+    j = json.loads(out.read_text())
+    assert [r["exchange"] for r in j["results"]] == ["buffered", "compact", "unbuffered"]
+    assert all(r["transforms_per_second"] > 0 for r in j["results"])
+    assert j["parameters"]["num_transforms"] == 2
+
+
+def test_bench_cli_mpi_r2c(tmp_path):
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = _run([MPIEXEC, "-n", "2", _prog("spfft_bench"), "-d", "20", "18", "16", "-r", "2",
+                "-o", "", "-e", "compactFloat", "-p", "cpu", "-t", "r2c", "-s", "0.6"])
+    assert "transforms/s" in out and "ranks: 2" in out
+
+
+@pytest.mark.gpu
+def test_bench_cli_gpu(gpu, tmp_path):
+    import json
+    out = tmp_path / "g.json"
+    _run([_prog("spfft_bench"), "-d", "64", "64", "64", "-r", "5", "-o", str(out), "-e", "compact",
+          "-p", "gpu-gpu", "--cutoff", "0.5"])
+    j = json.loads(out.read_text())
+    assert j["results"][0]["transforms_per_second"] > 0
