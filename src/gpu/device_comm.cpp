@@ -227,9 +227,17 @@ private:
   void barrier(hipStream_t stream) {
     SPFFT_TIMED_SCOPE("peer_barrier");
     DeviceGuard guard(device_);
-    dev::launch_peer_barrier(table_->data<unsigned long long*>(),
-                             static_cast<unsigned long long*>(flags_), me_, P_, ++epoch_, failDev_,
-                             timeoutTicks_, stream);
+    if (ipc_) {
+      dev::launch_peer_barrier(table_->data<unsigned long long*>(),
+                               static_cast<unsigned long long*>(flags_), me_, P_, ++epoch_,
+                               failDev_, timeoutTicks_, stream);
+    } else {
+      // ranks of one process share its few hardware queues: a spinning barrier
+      // kernel could sit in front of the very work it waits for, so in-process
+      // groups meet on the host instead
+      gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+      comm_->barrier();
+    }
     readPending_[0] = readPending_[1] = false;
   }
 

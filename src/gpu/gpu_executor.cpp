@@ -74,6 +74,11 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(colBase_, cb);
   upload(colX_, p.colX);
   upload(twX_, make_twiddles<T>(p.dimX));
+  // packed-real x stage for R2C with even dimX (SPFFT_R2C_PACKED=0 disables)
+  if (p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4 &&
+      env_int("SPFFT_R2C_PACKED", 1, 0, 1) && (dev::has_ct_kernel(p.dimX / 2) ||
+                                                p.dimX / 2 <= dev::max_device_fft_length(sizeof(T) == 8)))
+    upload(twXh_, make_twiddles<T>(p.dimX / 2));
   upload(twY_, make_twiddles<T>(p.dimY));
   upload(twZ_, make_twiddles<T>(p.dimZ));
 
@@ -346,7 +351,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
       dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
                                        twY_->data<cx<T>>(), stream_);
     dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space,
-                              twX_->data<cx<T>>(), stream_);
+                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
   }
   if (outputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
@@ -385,7 +390,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       ya.remote = 1;
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
-                             twX_->data<cx<T>>(), stream_);
+                             twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
     if (floatExchange_)
       dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
                                           twY_->data<cx<T>>(), stream_);

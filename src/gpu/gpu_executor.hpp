@@ -74,7 +74,7 @@ private:
   // hold those destinations as element offsets from the local buffer.
   bool peerWrites_ = false;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
-  std::unique_ptr<DeviceBuffer> twX_, twY_, twZ_;
+  std::unique_ptr<DeviceBuffer> twX_, twXh_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;
   std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;
 };

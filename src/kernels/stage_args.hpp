@@ -74,12 +74,14 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
 template <typename T, typename BT>
 void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* tw,
                       hipStream_t stream);
+// twHalf: length-n/2 twiddles; when given (R2C, even n) the packed-real
+// half-length kernels run instead of the hermitian-extended complex FFT.
 template <typename T>
 void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space, const cx<T>* tw,
-                       hipStream_t stream);
+                       const cx<T>* twHalf, hipStream_t stream);
 template <typename T>
 void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter, const cx<T>* tw,
-                      hipStream_t stream);
+                      const cx<T>* twHalf, hipStream_t stream);
 
 // Largest run-time FFT length supported in one workgroup (LDS-resident).
 int max_device_fft_length(bool doublePrecision);

@@ -13,6 +13,9 @@
 namespace spfft {
 namespace dev {
 
+#ifndef SPFFT_ROW_STAGE
+#define SPFFT_ROW_STAGE 1
+#endif
 #ifndef SPFFT_XB_DIRECT
 #define SPFFT_XB_DIRECT 0
 #endif
@@ -244,6 +247,21 @@ __device__ __forceinline__ void gather_to_lds(cx<T>* lds, int total, Load load, 
       }
     }
   }
+}
+
+// Row side of a line-fast kernel: lanes walk along rows (row-contiguous global
+// loads) into the FFT lines in LDS; line-fast lanes would touch B rows with
+// (64/B)-element segments per wave instruction (32 B segments for fp32 B=16).
+template <class Eng, typename T, class Load>
+__device__ __forceinline__ void stage_rows(const Eng& eng, cx<T>* lds, int rows, int len, Load load) {
+  gather_to_lds(lds, rows * len, [&](int idx) {
+    const int b = idx / len;
+    return load(b, idx - b * len);
+  }, [&](int idx) {
+    const int b = idx / len;
+    return eng.in_at(b, idx - b * len);
+  });
+  __syncthreads();
 }
 
 // Exclusive prefix sum of n ints in LDS (one wave, 64-wide shuffle scans); writes
@@ -598,13 +616,20 @@ __global__ void __launch_bounds__(kMaxThreads)
   }
   __syncthreads();
   const int zl = min(B, a.L - z0);
-  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+  auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
     return ld_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
-  }, [&](int b, int pos, cx<T> v) {
+  };
+  auto store = [&](int b, int pos, cx<T> v) {
     const int e = yEnt[pos];
     if (e >= 0 && b < zl) st_stream(&out[cBase[e] + b], cvt<typename BT::value_type>(v));
-  });
+  };
+#if SPFFT_ROW_STAGE
+  stage_rows(eng, lds, zl, n, load);
+  eng.lds_to_global(lds, tw, store);
+#else
+  eng.global_to_global(lds, tw, load, store);
+#endif
   release_remote(a.remote);
 }
 
@@ -679,15 +704,105 @@ __global__ void __launch_bounds__(kMaxThreads)
   __syncthreads();
   const int yl = min(B, a.Y - y0);
   cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
-  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+  auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
     if (R2C) return mk<T>(ld_stream_real(&static_cast<const T*>(space)[row + pos]), T(0));
     return ld_stream(&static_cast<const cx<T>*>(space)[row + pos]);
-  }, [&](int b, int pos, cx<T> v) {
+  };
+  auto store = [&](int b, int pos, cx<T> v) {
     const int c = xCol[pos];
     if (c >= 0 && b < yl) st_stream(&dst[static_cast<long long>(c) * a.interStride + b], v);
+  };
+#if SPFFT_ROW_STAGE
+  stage_rows(eng, lds, yl, n, load);
+  eng.lds_to_global(lds, tw, store);
+#else
+  eng.global_to_global(lds, tw, load, store);
+#endif
+}
+
+// Packed-real x stage (R2C transforms with even dimX): a real row of length n
+// is the complex sequence y[m] = x[2m] + i x[2m+1] of length h = n/2, so one
+// half-length FFT plus a twiddle pre-pass (C2R) or post-pass (R2C) replaces the
+// hermitian-extended length-n complex FFT: half the butterflies, half the LDS
+// traffic, and the real row is read/written as h contiguous complex values.
+//   C2R: Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k,  y = IDFT_h(Z)
+//   R2C: Y = DFT_h(y),  X[k] = (Y[k] + conj Y[h-k])/2 + w^k (Y[k] - conj Y[h-k])/(2i)
+// with w = exp(S 2 pi i / n); the imaginary parts of X[0] and X[h] are ignored
+// (they cannot contribute to a real signal), as in the complex C2R path.
+template <class Eng, typename T>
+__global__ void __launch_bounds__(kMaxThreads)
+    x_backward_c2r_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, T* __restrict__ space,
+                          const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
+  SPFFT_LDS_DECL(T);
+  const int B = eng.lines();
+  const int h = eng.n();
+  const long long n = 2 * static_cast<long long>(h);
+  const int zl = a.zBegin + blockIdx.y;
+  const int y0 = blockIdx.x * B;
+  int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int x = threadIdx.x; x <= h; x += blockDim.x) xCol[x] = -1;
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
+  __syncthreads();
+  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  const int yl = min(B, a.Y - y0);
+  auto at = [&](int k, int b) -> cx<T> {
+    const int c = xCol[k];
+    return c < 0 ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+  };
+  T* row0 = space + (static_cast<long long>(zl) * a.Y + y0) * n;
+  eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
+    if (b >= yl) return czero<T>();
+    cx<T> xk = at(k, b);
+    cx<T> xm = at(h - k, b);
+    if (k == 0) {
+      xk.y = T(0);
+      xm.y = T(0);
+    }
+    const cx<T> xmc = conj(xm);
+    return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twn[k]));
   });
+  // the yl rows are contiguous in the space domain: one coalesced copy-out
+  cx<T>* out = reinterpret_cast<cx<T>*>(row0);
+  for (int idx = threadIdx.x; idx < yl * h; idx += blockDim.x) {
+    const int b = idx / h, m = idx - b * h;
+    st_stream(&out[idx], lds[eng.out_at(b, m)]);
+  }
+}
+
+template <class Eng, typename T>
+__global__ void __launch_bounds__(kMaxThreads)
+    x_forward_r2c_kernel(Eng eng, XArgs a, const T* __restrict__ space, cx<T>* __restrict__ inter,
+                         const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
+  SPFFT_LDS_DECL(T);
+  const int B = eng.lines();
+  const int h = eng.n();
+  const long long n = 2 * static_cast<long long>(h);
+  const int zl = a.zBegin + blockIdx.y;
+  const int y0 = blockIdx.x * B;
+  int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  for (int x = threadIdx.x; x <= h; x += blockDim.x) xCol[x] = -1;
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
+  __syncthreads();
+  const int yl = min(B, a.Y - y0);
+  const cx<T>* row0 = reinterpret_cast<const cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
+  stage_rows(eng, lds, yl, h, [&](int b, int m) { return ld_stream(row0 + static_cast<long long>(b) * h + m); });
+  eng.lds_to_lds(lds, twh);
+  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  // post pass: lanes run over rows first, so the column stores are contiguous
+  for (int idx = threadIdx.x; idx < B * (h + 1); idx += blockDim.x) {
+    const int b = idx % B, k = idx / B;
+    const int c = xCol[k];
+    if (c < 0 || b >= yl) continue;
+    const cx<T> yk = lds[eng.out_at(b, k == h ? 0 : k)];
+    const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
+    const cx<T> e = scale(yk + ym, T(0.5));
+    const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
+    st_stream(&dst[static_cast<long long>(c) * a.interStride + b], e + twm<-1>(o, twn[k]));
+  }
 }
 
 // ------------------------------------------------------------ host helpers

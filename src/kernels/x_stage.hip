@@ -6,8 +6,19 @@ namespace dev {
 
 template <typename T>
 void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space,
-                       const cx<T>* tw, hipStream_t stream) {
+                       const cx<T>* tw, const cx<T>* twHalf, hipStream_t stream) {
   if (a.L <= a.zBegin || a.Y <= 0) return;
+  if (r2c && twHalf && a.n % 2 == 0 && a.n >= 4) {
+    with_engine<T, +1, true>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
+      auto k = x_backward_c2r_kernel<decltype(eng), T>;
+      const std::size_t ldsTotal = lds + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
+      prepare_kernel(k, ldsTotal);
+      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal,
+                         stream, eng, a, inter, static_cast<T*>(space), twHalf, tw);
+      gpu_check_launch("x_backward_c2r", stream);
+    });
+    return;
+  }
   with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_backward_kernel<decltype(eng), T, true> : x_backward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
@@ -20,8 +31,19 @@ void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space
 
 template <typename T>
 void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
-                      const cx<T>* tw, hipStream_t stream) {
+                      const cx<T>* tw, const cx<T>* twHalf, hipStream_t stream) {
   if (a.L <= a.zBegin || a.Y <= 0) return;
+  if (r2c && twHalf && a.n % 2 == 0 && a.n >= 4) {
+    with_engine<T, -1, true>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
+      auto k = x_forward_r2c_kernel<decltype(eng), T>;
+      const std::size_t ldsTotal = lds + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
+      prepare_kernel(k, ldsTotal);
+      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal,
+                         stream, eng, a, static_cast<const T*>(space), inter, twHalf, tw);
+      gpu_check_launch("x_forward_r2c", stream);
+    });
+    return;
+  }
   with_engine<T, -1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = r2c ? x_forward_kernel<decltype(eng), T, true> : x_forward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
@@ -33,13 +55,13 @@ void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
 }
 
 template void launch_x_backward<double>(const XArgs&, bool, const cx<double>*, void*,
-                                        const cx<double>*, hipStream_t);
+                                        const cx<double>*, const cx<double>*, hipStream_t);
 template void launch_x_backward<float>(const XArgs&, bool, const cx<float>*, void*,
-                                       const cx<float>*, hipStream_t);
+                                       const cx<float>*, const cx<float>*, hipStream_t);
 template void launch_x_forward<double>(const XArgs&, bool, const void*, cx<double>*,
-                                       const cx<double>*, hipStream_t);
+                                       const cx<double>*, const cx<double>*, hipStream_t);
 template void launch_x_forward<float>(const XArgs&, bool, const void*, cx<float>*,
-                                      const cx<float>*, hipStream_t);
+                                      const cx<float>*, const cx<float>*, hipStream_t);
 
 // ------------------------------------------------------------------ helpers
 RtPlan make_rt_plan(int n, std::size_t elemBytes) {

@@ -46,7 +46,8 @@ def test_c2c_sweep(gpu, dims, centered):
 
 
 @pytest.mark.parametrize("dims", [(8, 8, 8), (11, 12, 13), (16, 16, 32), (12, 11, 4), (2, 13, 11),
-                                  (256, 16, 16), (15, 64, 128)])
+                                  (256, 16, 16), (15, 64, 128), (4, 5, 6), (6, 7, 5), (200, 9, 8),
+                                  (1024, 4, 4)])
 def test_r2c(gpu, dims):
     import torch
     rng = np.random.default_rng(3)
@@ -59,6 +60,50 @@ def test_r2c(gpu, dims):
     assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < 1e-12
     out = t.backward(f)
     assert max_rel_error(out.cpu().numpy(), space * (nx * ny * nz)) < 1e-12
+
+
+@pytest.mark.parametrize("dims", [(16, 12, 10), (64, 32, 48), (30, 8, 9)])
+def test_r2c_sparse_columns_single(gpu, dims):
+    """Sparse R2C in fp32: x-columns present at k but absent at n/2-k exercise the
+    packed-real pre/post passes' zero handling."""
+    import torch
+    rng = np.random.default_rng(8)
+    nx, ny, nz = dims
+    idx = create_value_indices(rng, [1.0], 0.5, 0.8, nx, ny, nz, True)[0]
+    vals = dense_forward(rng.standard_normal((nz, ny, nx)), idx, dims).astype(np.complex64)
+    grid = sp.GridFloat(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C, nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    ref = dense_backward(idx, vals.astype(np.complex128), dims, r2c=True)
+    assert max_rel_error(out.cpu().numpy(), ref) < 2e-5
+    space = rng.standard_normal((nz, ny, nx)).astype(np.float32)
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space.astype(np.float64), idx, dims)) < 2e-5
+
+
+def test_r2c_sphere_256(gpu):
+    """Config 3 of BASELINE.json: 256^3 R2C spherical cutoff, fp64, vs torch.fft on the GPU."""
+    import torch
+    n = 256
+    dims = (n, n, n)
+    idx = sphere_indices(*dims, 0.5, r2c=True)
+    rng = np.random.default_rng(13)
+    space = torch.as_tensor(rng.standard_normal((n, n, n)), device=gpu)
+    grid = sp.Grid(n, n, n, n * n, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C, n, n, n, n, idx)
+    f = t.forward(space)
+    full = torch.fft.fftn(space.permute(2, 1, 0))  # [x][y][z]
+    s = torch.as_tensor(np.where(idx < 0, idx + n, idx).astype(np.int64), device=gpu)
+    ref = full[s[:, 0], s[:, 1], s[:, 2]]
+    err = (f - ref).abs().max() / ref.abs().max()
+    assert err.item() < 1e-12
+    # backward of a hermitian-consistent spectrum (the forward output) is real and exact
+    out = t.backward(f)
+    F = torch.zeros((n // 2 + 1, n, n), dtype=torch.complex128, device=gpu)
+    F[s[:, 0], s[:, 1], s[:, 2]] = f
+    ref_b = torch.fft.irfftn(F.permute(2, 1, 0), s=(n, n, n), dim=(0, 1, 2)) * n ** 3
+    err_b = (out - ref_b).abs().max() / ref_b.abs().max()
+    assert err_b.item() < 1e-11
 
 
 def test_r2c_half_plane_symmetry(gpu):

@@ -14,7 +14,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
 def build_variant(name, flags):
-    bdir = os.path.join(REPO, "build_var", name)
+    bdir = os.path.join(REPO, "build", "variants", name)
     clang = os.path.join(ROCM, "llvm", "bin")
     if not os.path.exists(os.path.join(bdir, "build.ninja")):
         subprocess.run(["cmake", "-S", REPO, "-B", bdir, "-G", "Ninja", "-DCMAKE_BUILD_TYPE=Release",
