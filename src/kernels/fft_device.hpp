@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fft/codelets.hpp"
 
 namespace spfft {
@@ -58,9 +60,9 @@ __host__ __device__ constexpr int padded_stride(int n) {
 
 // Lines per workgroup: as many as fit the LDS budget and the thread cap, with
 // the workgroup a whole number of waves.
-__host__ __device__ constexpr int lines_per_block(int tp, int lineBytes) {
+__host__ __device__ constexpr int lines_per_block(int tp, int lineBytes, int budget = kLdsBudget) {
   int b = kMaxThreads / tp;
-  if (b * lineBytes > kLdsBudget) b = kLdsBudget / lineBytes;
+  if (b * lineBytes > budget) b = budget / lineBytes;
   if (b < 1) b = 1;
   if (tp < 64) {
     const int q = 64 / tp;
@@ -113,6 +115,31 @@ struct CtShape<1024> {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 4;
 };
 
+// Shape per precision: E is raised where the default would leave the line-fast
+// mapping fewer lines than one 128-byte column segment needs (8 lines of
+// complex<double>, 16 of complex<float>); those shapes get an 80 KB LDS budget
+// (two workgroups per CU).
+template <typename T, int N>
+struct CtShapeT : CtShape<N> {
+  static constexpr int kBudget = kLdsBudget;
+};
+template <int N>
+struct CtShapeT<void, N> : CtShape<N> {
+  static constexpr int kBudget = kLdsBudget;
+};
+template <>
+struct CtShapeT<double, 512> {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024;
+};
+template <>
+struct CtShapeT<float, 512> {
+  static constexpr int E = 32, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024;
+};
+template <>
+struct CtShapeT<float, 1024> {
+  static constexpr int E = 32, R0 = 16, R1 = 16, R2 = 4, kBudget = 80 * 1024;
+};
+
 struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 
 // largest power of two <= b, at most 16 (line-fast lane mapping)
@@ -149,11 +176,13 @@ __host__ __device__ constexpr int lf_padded_stride(int n, int b) {
 //         stick's z-run or an intermediate column's y-run).
 template <typename T, int N, int S, bool LF = false>
 struct FftCT {
-  using Sh = CtShape<N>;
+  // line-fast engines (column access) take the precision-specific shape; the
+  // row-mapped engine of the z stage keeps the default (fewer VGPRs per lane)
+  using Sh = typename std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::type;
   static constexpr int E = Sh::E;
   static constexpr int TP = N / E;  // lanes per line
   static constexpr int LS0 = padded_stride<T>(N);
-  static constexpr int B0 = lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)));
+  static constexpr int B0 = lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), Sh::kBudget);
   static constexpr int B = LF ? lf_lines(B0) : B0;
   static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B) : LS0;
   static constexpr int NT = B * TP;

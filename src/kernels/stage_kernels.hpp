@@ -741,31 +741,48 @@ __global__ void __launch_bounds__(kMaxThreads)
   const long long n = 2 * static_cast<long long>(h);
   const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
-  int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  // LDS: FFT lines | X[h] (Nyquist) per line | xCol table
+  cx<T>* nyq = reinterpret_cast<cx<T>*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+  int* xCol = reinterpret_cast<int*>(nyq + B);
   for (int x = threadIdx.x; x <= h; x += blockDim.x) xCol[x] = -1;
   __syncthreads();
   for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
   __syncthreads();
   const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   const int yl = min(B, a.Y - y0);
-  auto at = [&](int k, int b) -> cx<T> {
+  // columns X[0..h] of the block's rows, each element loaded once (lanes run
+  // over rows: contiguous column segments)
+  gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
+    const int k = idx / B, b = idx - k * B;
     const int c = xCol[k];
-    return c < 0 ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
-  };
-  T* row0 = space + (static_cast<long long>(zl) * a.Y + y0) * n;
-  eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
-    if (b >= yl) return czero<T>();
-    cx<T> xk = at(k, b);
-    cx<T> xm = at(h - k, b);
+    return (c < 0 || b >= yl) ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+  }, [&](int idx) {
+    const int k = idx / B;
+    return eng.in_at(idx - k * B, k);
+  });
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int c = xCol[h];
+    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+  }
+  __syncthreads();
+  // pre-pass in place, pairs (k, h-k): Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k
+  for (int idx = threadIdx.x; idx < B * (h / 2 + 1); idx += blockDim.x) {
+    const int k = idx / B, b = idx - k * B;
+    const int m = h - k;
+    cx<T> xk = lds[eng.in_at(b, k)];
+    cx<T> xm = m == h ? nyq[b] : lds[eng.in_at(b, m)];
     if (k == 0) {
       xk.y = T(0);
       xm.y = T(0);
     }
-    const cx<T> xmc = conj(xm);
-    return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twn[k]));
-  });
+    const cx<T> xmc = conj(xm), xkc = conj(xk);
+    lds[eng.in_at(b, k)] = (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twn[k]));
+    if (m != k && m < h) lds[eng.in_at(b, m)] = (xm + xkc) + rot<+1>(twm<+1>(xm - xkc, twn[m]));
+  }
+  __syncthreads();
+  eng.lds_to_lds(lds, twh);
   // the yl rows are contiguous in the space domain: one coalesced copy-out
-  cx<T>* out = reinterpret_cast<cx<T>*>(row0);
+  cx<T>* out = reinterpret_cast<cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
   for (int idx = threadIdx.x; idx < yl * h; idx += blockDim.x) {
     const int b = idx / h, m = idx - b * h;
     st_stream(&out[idx], lds[eng.out_at(b, m)]);

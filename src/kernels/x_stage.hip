@@ -11,7 +11,8 @@ void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space
   if (r2c && twHalf && a.n % 2 == 0 && a.n >= 4) {
     with_engine<T, +1, true>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
       auto k = x_backward_c2r_kernel<decltype(eng), T>;
-      const std::size_t ldsTotal = lds + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
+      const std::size_t ldsTotal =
+          lds + std::size_t(lines) * sizeof(cx<T>) + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
       prepare_kernel(k, ldsTotal);
       hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal,
                          stream, eng, a, inter, static_cast<T*>(space), twHalf, tw);
