@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 
 #include "core/timing.hpp"
 #include "fft/fft_plan.hpp"
@@ -93,7 +94,112 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     // collective data-plane setup happens at plan time
     peerWrites_ = grid_->device_comm().peer_writes();
     if (peerWrites_) build_peer_tables();
+    // exchange pipelining: chunk count agreed on every rank (rank 0's choice)
+    int chunks = env_int("SPFFT_EXCH_CHUNKS", 4, 1, 64);
+    std::vector<int> all(p.size);
+    grid_->communicator()->allgather(&chunks, all.data(), sizeof(int));
+    chunks = all[0];
+    if (!peerWrites_ && chunkPlanes_ == 0 && chunks > 1) build_chunk_plan(chunks);
   }
+}
+
+template <typename T>
+void GpuExecutor<T>::build_chunk_plan(int K) {
+  const IndexPlan& p = *plan_;
+  const int P = p.size, me = p.rank;
+  const std::int64_t eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+  // K depends on global quantities only: every rank issues the same number of
+  // all-to-all rounds (ranks with few sticks get empty chunks)
+  const int ncols = p.num_columns();
+  if (ncols < 1) return;
+  K = std::max(1, std::min(K, ncols));
+  // backward: chunk k = sticks [S_q k / K, S_q (k+1) / K) of every rank q
+  auto sb = [&](int q, int k) { return static_cast<std::int64_t>(p.sticksPerRank[q]) * k / K; };
+  bwdStickBounds_.resize(K + 1);
+  for (int k = 0; k <= K; ++k) bwdStickBounds_[k] = static_cast<int>(sb(me, k));
+  bwdChunks_.assign(K, ChunkXfer{});
+  for (int k = 0; k < K; ++k) {
+    ChunkXfer& c = bwdChunks_[k];
+    for (int r = 0; r < P; ++r) {
+      const std::int64_t s0 = sb(me, k), s1 = sb(me, k + 1);
+      c.sd.push_back((layout_.stickDispl[r] + s0 * layout_.stickStride[r]) * eb);
+      c.sc.push_back((s1 - s0) * layout_.stickStride[r] * eb);
+      const std::int64_t q0 = sb(r, k), q1 = sb(r, k + 1);
+      c.rd.push_back((layout_.slabDispl[r] + q0 * layout_.slabStride) * eb);
+      c.rc.push_back((q1 - q0) * layout_.slabStride * eb);
+    }
+  }
+  // forward: chunk k = columns [cb_k, cb_{k+1}) balanced by stick entries; every
+  // rank's sticks inside a column range are a contiguous run of its local sticks
+  // (columns ascend in x, local sticks ascend in x*dimY+y)
+  fwdColBounds_.assign(K + 1, ncols);
+  fwdColBounds_[0] = 0;
+  const std::int64_t total = p.colOffsets[ncols];
+  for (int k = 1; k < K; ++k) {
+    int c = fwdColBounds_[k - 1];
+    while (c < ncols && static_cast<std::int64_t>(p.colOffsets[c]) * K < total * k) ++c;
+    fwdColBounds_[k] = c;
+  }
+  std::vector<std::vector<std::int64_t>> rowB(K, std::vector<std::int64_t>(P, 0)),
+      rowE(K, std::vector<std::int64_t>(P, 0));
+  for (int k = 0; k < K; ++k) {
+    std::vector<std::int64_t> lo(P, std::numeric_limits<std::int64_t>::max()), hi(P, -1), cnt(P, 0);
+    for (int e = p.colOffsets[fwdColBounds_[k]]; e < p.colOffsets[fwdColBounds_[k + 1]]; ++e) {
+      const int r = p.colRank[e];
+      lo[r] = std::min<std::int64_t>(lo[r], p.colLocal[e]);
+      hi[r] = std::max<std::int64_t>(hi[r], p.colLocal[e]);
+      ++cnt[r];
+    }
+    for (int r = 0; r < P; ++r) {
+      if (cnt[r] == 0) continue;
+      if (hi[r] - lo[r] + 1 != cnt[r]) {  // not contiguous: no forward pipelining
+        fwdColBounds_.clear();
+        break;
+      }
+      rowB[k][r] = lo[r];
+      rowE[k][r] = hi[r] + 1;
+    }
+    if (fwdColBounds_.empty()) break;
+  }
+  if (!fwdColBounds_.empty()) {
+    fwdChunks_.assign(K, ChunkXfer{});
+    for (int k = 0; k < K; ++k) {
+      ChunkXfer& c = fwdChunks_[k];
+      for (int r = 0; r < P; ++r) {
+        // send: my slab-side rows of rank r's sticks in this column chunk
+        c.sd.push_back((layout_.slabDispl[r] + rowB[k][r] * layout_.slabStride) * eb);
+        c.sc.push_back((rowE[k][r] - rowB[k][r]) * layout_.slabStride * eb);
+        // receive: my sticks' rows of this chunk from every rank
+        c.rd.push_back((layout_.stickDispl[r] + rowB[k][me] * layout_.stickStride[r]) * eb);
+        c.rc.push_back((rowE[k][me] - rowB[k][me]) * layout_.stickStride[r] * eb);
+      }
+    }
+  }
+  exchChunks_ = K;
+  commStream_.reset(new GpuStream());
+  chunkEvents_.clear();
+  for (int k = 0; k < K; ++k) chunkEvents_.emplace_back(new GpuEvent());
+  commDone_.reset(new GpuEvent());
+}
+
+template <typename T>
+void GpuExecutor<T>::pipelined_exchange(bool backward) {
+  DeviceGuard guard(deviceId_);
+  void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
+  DeviceComm& dc = grid_->device_comm();
+  hipStream_t cs = commStream_->get();
+  const auto& chunks = backward ? bwdChunks_ : fwdChunks_;
+  for (int k = 0; k < exchChunks_; ++k) {
+    chunkEvents_[k]->wait_on(cs);
+    const ChunkXfer& c = chunks[k];
+    if (backward)
+      dc.alltoallv(stick, c.sc.data(), c.sd.data(), slab, c.rc.data(), c.rd.data(), cs);
+    else
+      dc.alltoallv(slab, c.sc.data(), c.sd.data(), stick, c.rc.data(), c.rd.data(), cs);
+  }
+  commDone_->record(cs);
+  commDone_->wait_on(stream_);
 }
 
 template <typename T>
@@ -220,6 +326,7 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
   const IndexPlan& p = *plan_;
   dev::ZArgs a{};
   a.numSticks = p.local_sticks();
+  a.stickBegin = 0;
   a.n = p.dimZ;
   a.zeroStick = p.type == SPFFT_TRANS_R2C ? p.zeroStick : -1;
   a.runs = runs_ ? runs_->data<StickRun>() : nullptr;
@@ -239,6 +346,8 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   const IndexPlan& p = *plan_;
   dev::YArgs a{};
   a.ncols = p.num_columns();
+  a.colBegin = 0;
+  a.colEnd = a.ncols;
   a.L = p.local_planes();
   a.zBegin = 0;
   a.n = p.dimY;
@@ -291,12 +400,20 @@ void GpuExecutor<T>::backward_z(const T* input) {
     a.segDispl = segDisplRemote_->data<long long>();
     a.remote = 1;
   }
-  if (floatExchange_)
-    dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
-                                         twZ_->data<cx<T>>(), stream_);
-  else
-    dev::launch_z_backward<T, cx<T>>(a, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
-                                     stream_);
+  const bool chunked = exchChunks_ > 1 && !bwdChunks_.empty();
+  for (int k = 0; k < (chunked ? exchChunks_ : 1); ++k) {
+    if (chunked) {
+      a.stickBegin = bwdStickBounds_[k];
+      a.numSticks = bwdStickBounds_[k + 1];
+    }
+    if (floatExchange_)
+      dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
+                                           twZ_->data<cx<T>>(), stream_);
+    else
+      dev::launch_z_backward<T, cx<T>>(a, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
+                                       stream_);
+    if (chunked) chunkEvents_[k]->record(stream_);
+  }
 }
 
 template <typename T>
@@ -320,6 +437,10 @@ void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
+    return;
+  }
+  if (exchChunks_ > 1 && !bwdChunks_.empty()) {
+    pipelined_exchange(true);
     return;
   }
   exchange(true);
@@ -391,12 +512,22 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
-    if (floatExchange_)
-      dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
-                                          twY_->data<cx<T>>(), stream_);
-    else
-      dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab),
-                                      twY_->data<cx<T>>(), stream_);
+    // column chunks of the pipelined exchange (chunk k's all-to-all starts when
+    // its y stage is done)
+    const bool chunked = exchChunks_ > 1 && !fwdChunks_.empty();
+    for (int k = 0; k < (chunked ? exchChunks_ : 1); ++k) {
+      if (chunked) {
+        ya.colBegin = fwdColBounds_[k];
+        ya.colEnd = fwdColBounds_[k + 1];
+      }
+      if (floatExchange_)
+        dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+                                            twY_->data<cx<T>>(), stream_);
+      else
+        dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab),
+                                        twY_->data<cx<T>>(), stream_);
+      if (chunked) chunkEvents_[k]->record(stream_);
+    }
   }
 }
 
@@ -406,6 +537,10 @@ void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
+    return;
+  }
+  if (exchChunks_ > 1 && !fwdChunks_.empty()) {
+    pipelined_exchange(false);
     return;
   }
   exchange(false);

@@ -45,6 +45,8 @@ private:
   void order_after_default_stream();
   void exchange(bool backward);
   void build_peer_tables();
+  void build_chunk_plan(int chunks);
+  void pipelined_exchange(bool backward);
   void wait_stream();
   dev::ZArgs zargs() const;
   dev::YArgs yargs() const;
@@ -74,6 +76,19 @@ private:
   // hold those destinations as element offsets from the local buffer.
   bool peerWrites_ = false;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
+
+  // Pipelined exchange (RCCL / loopback data planes): the z stage (backward) and
+  // the y stage (forward) run in K chunks of sticks / columns; chunk k's
+  // all-to-all runs on commStream_ while chunk k+1 is computed.
+  struct ChunkXfer {
+    std::vector<std::int64_t> sc, sd, rc, rd;  // bytes per rank
+  };
+  int exchChunks_ = 1;
+  std::vector<int> bwdStickBounds_, fwdColBounds_;
+  std::vector<ChunkXfer> bwdChunks_, fwdChunks_;
+  std::unique_ptr<GpuStream> commStream_;
+  std::vector<std::unique_ptr<GpuEvent>> chunkEvents_;
+  std::unique_ptr<GpuEvent> commDone_;
   std::unique_ptr<DeviceBuffer> twX_, twXh_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;
   std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;

@@ -21,7 +21,8 @@ namespace spfft {
 namespace dev {
 
 struct ZArgs {
-  int numSticks;
+  int numSticks;   // end of the stick range processed (exclusive)
+  int stickBegin;  // first stick of the range (exchange pipelining chunks)
   int n;          // dimZ
   int zeroStick;  // line to hermitian-fill (R2C backward), -1 for none
   const StickRun* runs;
@@ -37,7 +38,9 @@ struct ZArgs {
 };
 
 struct YArgs {
-  int ncols;
+  int ncols;     // columns of the [z][column][y] intermediate (its row count per plane)
+  int colBegin;  // column range processed: [colBegin, colEnd) (exchange pipelining chunks)
+  int colEnd;
   int L;       // end of the plane range processed (exclusive; = local planes)
   int zBegin;  // first plane of the range (plane chunking)
   int n;  // dimY

@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(kMaxThreads)
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const int s0 = blockIdx.x * B;
+  const int s0 = a.stickBegin + blockIdx.x * B;
   zero_lds(lds, eng.input_elems());
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(kMaxThreads)
                      T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const int s0 = blockIdx.x * B;
+  const int s0 = a.stickBegin + blockIdx.x * B;
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int s0 = blockIdx.x * B;
+  const int s0 = a.stickBegin + blockIdx.x * B;
   const int nl = min(B, a.numSticks - s0);
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(kMaxThreads)
                           T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const int s0 = blockIdx.x * B;
+  const int s0 = a.stickBegin + blockIdx.x * B;
   const int nl = min(B, a.numSticks - s0);
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -537,7 +537,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = blockIdx.x;
+  const int c = a.colBegin + blockIdx.x;
   const int z0 = a.zBegin + blockIdx.y * B;
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
@@ -602,7 +602,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = blockIdx.x;
+  const int c = a.colBegin + blockIdx.x;
   const int z0 = a.zBegin + blockIdx.y * B;
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;

@@ -7,12 +7,12 @@ namespace dev {
 template <typename T, typename BT>
 void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* tw,
                        hipStream_t stream) {
-  if (a.ncols <= 0 || a.L <= a.zBegin) return;
+  if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
   with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = y_backward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(a.ncols, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        in, inter, tw);
     gpu_check_launch("y_backward", stream);
   });
@@ -21,12 +21,12 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
 template <typename T, typename BT>
 void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* tw,
                       hipStream_t stream) {
-  if (a.ncols <= 0 || a.L <= a.zBegin) return;
+  if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
   with_engine<T, -1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = y_forward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * (sizeof(long long) + sizeof(int)) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(a.ncols, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        inter, out, tw);
     gpu_check_launch("y_forward", stream);
   });

@@ -8,13 +8,13 @@ namespace dev {
 template <typename T, typename BT>
 void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>* tw,
                        hipStream_t stream) {
-  if (a.numSticks <= 0) return;
+  if (a.numSticks <= a.stickBegin) return;
   with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = a.desc ? z_backward_desc_kernel<decltype(eng), T, BT>
                     : z_backward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        values, out, tw);
     gpu_check_launch("z_backward", stream);
   });
@@ -23,13 +23,13 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
 template <typename T, typename BT>
 void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, const cx<T>* tw,
                       hipStream_t stream) {
-  if (a.numSticks <= 0) return;
+  if (a.numSticks <= a.stickBegin) return;
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = a.desc ? z_forward_desc_kernel<decltype(eng), T, BT>
                     : z_forward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
                        in, values, scale, tw);
     gpu_check_launch("z_forward", stream);
   });

@@ -244,3 +244,60 @@ def test_user_stream_async(gpu):
         out = t.forward(None, scaling=sp.Scaling.FULL)
     t.synchronize()
     assert (out - vals).abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 8])
+@pytest.mark.parametrize("dist", ["uniform", "rank0", "rank0_planes_last", "r2c"])
+def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, monkeypatch):
+    """Reference distribution sweep (tests/mpi_tests/test_transform.cpp) on P=3 virtual
+    ranks of one GPU, through the pipelined exchange with 1, 3 and 8 chunks (ranks
+    with few or no sticks get empty chunks; every rank issues the same rounds)."""
+    import torch
+    from spfft_amd.parallel import run_ranks
+    from spfft_amd.utils.indices import calculate_num_local_xy_planes
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    dims = (20, 18, 17)
+    nx, ny, nz = dims
+    P = 3
+    r2c = dist == "r2c"
+    stick_dist = {"uniform": [1, 1, 1], "rank0": [1, 0, 0], "rank0_planes_last": [1, 0, 0],
+                  "r2c": [1, 2, 1]}[dist]
+    plane_dist = {"uniform": [1, 1, 1], "rank0": [1, 0, 0], "rank0_planes_last": [0, 0, 1],
+                  "r2c": [1, 1, 1]}[dist]
+    rng = np.random.default_rng(21)
+    parts = create_value_indices(rng, stick_dist, 0.7, 0.8, nx, ny, nz, r2c)
+    planes = [calculate_num_local_xy_planes(r, nz, plane_dist) for r in range(P)]
+    offsets = np.concatenate([[0], np.cumsum(planes)])
+    all_idx = np.concatenate(parts)
+    space = rng.standard_normal((nz, ny, nx))
+    if r2c:
+        vals_all = dense_forward(space, all_idx, dims, r2c=True)
+    else:
+        vals_all = _rand_vals(rng, len(all_idx))
+    ref = dense_backward(all_idx, vals_all, dims, r2c=r2c)
+    field = space if r2c else space + 1j * rng.standard_normal((nz, ny, nx))
+    ref_fwd = dense_forward(field, all_idx, dims, r2c=r2c)
+    starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
+    ttype = sp.TransformType.R2C if r2c else sp.TransformType.C2C
+    max_sticks = max(len(np.unique(p[:, 0] * ny + p[:, 1])) if len(p) else 0 for p in parts)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        grid = sp.Grid(nx, ny, nz, max(1, max_sticks), GPU, 1, max_local_z_length=max(planes),
+                       comm=comm, exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+        t = grid.create_transform(GPU, ttype, nx, ny, nz, planes[rank], parts[rank])
+        v = torch.as_tensor(vals_all[starts[rank]:starts[rank + 1]], device="cuda")
+        errs = []
+        for _ in range(2):
+            out = t.backward(v).cpu().numpy()
+            errs.append(max_rel_error(out, ref[offsets[rank]:offsets[rank + 1]]) if planes[rank]
+                        else 0.0)
+        # forward of this rank's slab of a known field
+        slab = torch.as_tensor(np.ascontiguousarray(field[offsets[rank]:offsets[rank + 1]]),
+                               device="cuda")
+        f = t.forward(slab).cpu().numpy()
+        errs.append(max_rel_error(f, ref_fwd[starts[rank]:starts[rank + 1]]) if len(f) else 0.0)
+        return max(errs)
+
+    for e in run_ranks(P, body):
+        assert e < 1e-11
