@@ -44,6 +44,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
   chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
+  poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
@@ -374,12 +375,36 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   return a;
 }
 
+// NaN poisoning (debug aid, generalises the reference tests' "run twice"):
+// every work buffer a direction writes before reading is filled with NaN bytes
+// first, so a kernel that reads an element nobody wrote shows up as NaN output.
+template <typename T>
+void GpuExecutor<T>::poison(bool backward) {
+  if (!poison_) return;
+  auto fill = [&](typename GridImpl<T>::Slot slot) {
+    gpu_check(hipMemsetAsync(grid_->device_slot(slot), 0xFF,
+                             static_cast<std::size_t>(grid_->slot_elements(slot)) * sizeof(cx<T>),
+                             stream_),
+              "hipMemsetAsync");
+  };
+  fill(GridImpl<T>::kInter);
+  if (backward) {
+    fill(GridImpl<T>::kSpace);
+    if (plan_->size == 1 || !peerWrites_) fill(GridImpl<T>::kStickSide);
+    if (plan_->size == 1) fill(GridImpl<T>::kSlabSide);
+  } else if (plan_->size == 1) {
+    fill(GridImpl<T>::kStickSide);
+    fill(GridImpl<T>::kSlabSide);
+  }
+}
+
 // ------------------------------------------------------------------ backward
 template <typename T>
 void GpuExecutor<T>::backward_z(const T* input) {
   SPFFT_TIMED_SCOPE("gpu_backward_z");
   DeviceGuard guard(deviceId_);
   order_after_default_stream();
+  poison(true);
   const IndexPlan& p = *plan_;
   const cx<T>* values = reinterpret_cast<const cx<T>*>(input);
   if (p.numLocalElements > 0) {
@@ -495,6 +520,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
                              hipMemcpyHostToDevice, stream_),
               "hipMemcpyAsync");
   }
+  poison(false);
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides

@@ -48,6 +48,7 @@ private:
   void build_chunk_plan(int chunks);
   void pipelined_exchange(bool backward);
   void wait_stream();
+  void poison(bool backward);
   dev::ZArgs zargs() const;
   dev::YArgs yargs() const;
   dev::XArgs xargs() const;
@@ -60,6 +61,7 @@ private:
   bool floatExchange_ = false;
   long long interStride_ = 0;  // row stride of [z][column][y]
   int chunkPlanes_ = 0;        // y/x stages interleaved per chunk of planes (0 = off)
+  bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;
 
   std::unique_ptr<GpuStream> ownStream_;

@@ -1,6 +1,7 @@
 #include "host/host_executor.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/timing.hpp"
@@ -189,9 +190,26 @@ void HostExecutor<T>::z_forward(const BT* stick, cx<T>* values, T factor) {
 }
 
 // ------------------------------------------------------------------ stages
+// SPFFT_POISON=1: NaN-fill the work buffers a direction writes before reading
+// them (debug aid; see GpuExecutor::poison).
+template <typename T>
+void HostExecutor<T>::poison(bool backward) {
+  const char* env = std::getenv("SPFFT_POISON");
+  if (!env || env[0] != '1') return;
+  auto fill = [&](typename GridImpl<T>::Slot slot) {
+    std::memset(grid_->host_slot(slot), 0xFF,
+                static_cast<std::size_t>(grid_->slot_elements(slot)) * sizeof(cx<T>));
+  };
+  fill(GridImpl<T>::kStickSide);
+  fill(GridImpl<T>::kInter);
+  if (plan_->size > 1) fill(GridImpl<T>::kSlabSide);
+  if (backward) fill(GridImpl<T>::kSpace);
+}
+
 template <typename T>
 void HostExecutor<T>::backward_z(const T* input) {
   SPFFT_TIMED_SCOPE("backward_z");
+  poison(true);
   void* stick = grid_->host_slot(GridImpl<T>::kStickSide);
   const auto* values = reinterpret_cast<const cx<T>*>(input);
   if (plan_->numLocalElements > 0 && !input) throw InvalidParameterError();
@@ -246,6 +264,7 @@ void HostExecutor<T>::backward_xy() {
 template <typename T>
 void HostExecutor<T>::forward_xy() {
   SPFFT_TIMED_SCOPE("forward_xy");
+  poison(false);
   const bool dist = plan_->size > 1;
   auto* inter = static_cast<cx<T>*>(grid_->host_slot(GridImpl<T>::kInter));
   x_forward(space_domain(), inter);

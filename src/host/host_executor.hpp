@@ -41,6 +41,7 @@ private:
   void x_backward(const cx<T>* inter, T* space);
   void x_forward(const T* space, cx<T>* inter);
   void exchange(bool backward);
+  void poison(bool backward);
   cx<T>* scratch(int thread, std::size_t n);
 
   std::shared_ptr<GridImpl<T>> grid_;

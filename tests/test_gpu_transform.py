@@ -301,3 +301,30 @@ def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, monkeypatch):
 
     for e in run_ranks(P, body):
         assert e < 1e-11
+
+
+@pytest.mark.parametrize("dims,ttype", [((16, 12, 20), "c2c"), ((11, 13, 12), "c2c"),
+                                        ((16, 10, 14), "r2c"), ((15, 8, 9), "r2c"),
+                                        ((64, 64, 64), "c2c")])
+def test_nan_poison(gpu, dims, ttype, monkeypatch):
+    """SPFFT_POISON=1 fills every work buffer with NaN before each direction: a kernel
+    reading an element no stage wrote would leak NaN into the result."""
+    import torch
+    monkeypatch.setenv("SPFFT_POISON", "1")
+    rng = np.random.default_rng(17)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.6, 0.6, nx, ny, nz, r2c)[0]
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    vals = dense_forward(space, idx, dims, r2c=r2c)
+    grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    assert not torch.isnan(out).any()
+    assert max_rel_error(out.cpu().numpy(), dense_backward(idx, vals, dims, r2c=r2c)) < 1e-12
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert not torch.isnan(f).any()
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims, r2c=r2c)) < 1e-12
