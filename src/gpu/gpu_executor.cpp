@@ -95,8 +95,15 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     // collective data-plane setup happens at plan time
     peerWrites_ = grid_->device_comm().peer_writes();
     if (peerWrites_) build_peer_tables();
-    // exchange pipelining: chunk count agreed on every rank (rank 0's choice)
-    int chunks = env_int("SPFFT_EXCH_CHUNKS", 4, 1, 64);
+    // exchange pipelining. Automatic choice: chunks only while the average
+    // per-peer message of a chunk stays >= 4 MB (smaller RCCL messages lose
+    // more link efficiency than the overlap gains), at most 4; computed from
+    // global quantities so every rank agrees. SPFFT_EXCH_CHUNKS forces a count
+    // (rank 0's value is used everywhere).
+    const double perPeer = static_cast<double>(p.totalSticks) * p.dimZ * eb /
+                           (static_cast<double>(p.size) * p.size);
+    int chunks = static_cast<int>(std::min(4.0, std::max(1.0, std::floor(perPeer / (4 << 20)))));
+    chunks = env_int("SPFFT_EXCH_CHUNKS", chunks, 1, 64);
     std::vector<int> all(p.size);
     grid_->communicator()->allgather(&chunks, all.data(), sizeof(int));
     chunks = all[0];
