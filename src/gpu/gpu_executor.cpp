@@ -84,6 +84,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(twY_, make_twiddles<T>(p.dimY));
   upload(twZ_, make_twiddles<T>(p.dimZ));
 
+  if (!distributed) setup_fused();
+
   if (distributed) {
     const std::int64_t eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
     for (int r = 0; r < p.size; ++r) {
@@ -255,8 +257,81 @@ GpuExecutor<T>::~GpuExecutor() {
   try {
     DeviceGuard guard(deviceId_);
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (fusedFailHost_) (void)hipHostFree(fusedFailHost_);
   } catch (...) {
   }
+}
+
+template <typename T>
+void GpuExecutor<T>::setup_fused() {
+  const IndexPlan& p = *plan_;
+  if (p.size != 1 || p.type != SPFFT_TRANS_C2C || !p.simpleSticks || chunkPlanes_ != 0) return;
+  // opt-in (SPFFT_FUSED=1): measured slower than the three-kernel path on MI355X
+  // (profiles/README.md, "fused y/x experiment")
+  if (!env_int("SPFFT_FUSED", 0, 0, 1) || !dev::fused_supported(p.dimX, p.dimY, p.dimZ)) return;
+  const int S = p.local_sticks(), ncols = p.num_columns();
+  if (S < 1 || ncols < 1) return;
+  for (std::size_t e = 0; e < p.colLocal.size(); ++e)
+    if (p.colLocal[e] != static_cast<int>(e)) return;  // entries must be the stick order
+  const long long Sp = S + env_int("SPFFT_PAD_STICK", 8, 0, kMaxPad);
+  if (static_cast<long long>(p.dimZ) * Sp > grid_->slot_elements(GridImpl<T>::kStickSide)) return;
+  int cus = 0;
+  gpu_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, deviceId_),
+            "hipDeviceGetAttribute");
+  const int bpc = std::min(2, dev::fused_blocks_per_cu<T>(p.dimX, p.dimY));
+  if (cus < 1 || bpc < 1) return;
+  std::vector<int> entryCol(p.colY.size());
+  for (int c = 0; c < ncols; ++c)
+    for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e) entryCol[e] = c;
+  upload(entryCol_, entryCol);
+  const int lag = env_int("SPFFT_FUSED_LAG", 2, 1, dev::kMaxRing - 1);
+  const int ring = std::max(lag + 1, env_int("SPFFT_FUSED_RING", lag + 2, 2, dev::kMaxRing));
+  const long long stride = ncols + 8;
+  fscratch_.reset(new DeviceBuffer(static_cast<std::size_t>(8) * ring * p.dimY * stride * sizeof(cx<T>)));
+  fctrl_.reset(new DeviceBuffer(dev::kFusedCtrlWords * sizeof(unsigned)));
+  gpu_check(hipHostMalloc(reinterpret_cast<void**>(&fusedFailHost_), 64,
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc");
+  *fusedFailHost_ = 0;
+  unsigned* failDev = nullptr;
+  gpu_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev), fusedFailHost_, 0),
+            "hipHostGetDevicePointer");
+  int rateKHz = 0;
+  gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, deviceId_),
+            "hipDeviceGetAttribute");
+  dev::FusedArgs& a = fargs_;
+  a.S = S;
+  a.Sp = Sp;
+  a.X = p.dimX;
+  a.Y = p.dimY;
+  a.Z = p.dimZ;
+  a.ncols = ncols;
+  a.colOffsets = colOffsets_->data<int>();
+  a.colY = colY_->data<int>();
+  a.colX = colX_->data<int>();
+  a.entryCol = entryCol_->data<int>();
+  a.desc = descs_->data<StickDesc>();
+  a.scratchStride = stride;
+  a.scratchPlane = static_cast<long long>(p.dimY) * stride;
+  a.ring = ring;
+  a.lag = lag;
+  a.debug = env_int("SPFFT_FUSED_DEBUG", 0, 0, 255);
+  a.ctrl = fctrl_->data<unsigned>();
+  a.failure = failDev;
+  a.timeout = static_cast<long long>(2.0 * 1e3 * std::max(rateKHz, 1));  // 2 s
+  fusedGrid_ = cus * bpc;
+  fused_ = true;
+}
+
+template <typename T>
+void GpuExecutor<T>::check_fused() {
+  if (!fusedFailHost_ || __atomic_load_n(fusedFailHost_, __ATOMIC_ACQUIRE) == 0) return;
+  // a persistent kernel could not synchronise its workgroups (grid not resident,
+  // e.g. a shared GPU): results of that call are invalid; fall back for good
+  *fusedFailHost_ = 0;
+  fused_ = false;
+  set_error_detail("fused y/x kernel: workgroup synchronisation timed out; fused path disabled");
+  throw GPUError();
 }
 
 template <typename T>
@@ -278,6 +353,7 @@ void GpuExecutor<T>::synchronize() {
   wait_stream();
   // a peer barrier that timed out leaves a flag behind (data are incomplete)
   if (peerWrites_) grid_->device_comm().check();
+  check_fused();
 }
 
 template <typename T>
@@ -425,6 +501,11 @@ void GpuExecutor<T>::backward_z(const T* input) {
     }
   }
   void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
+  if (fused_) {
+    dev::launch_z_backward_pm<T>(fargs_, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
+                                 stream_);
+    return;
+  }
   auto a = zargs();
   if (peerWrites_) {
     // the z stage stores straight into the peers' slab sides
@@ -488,6 +569,20 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
+  if (fused_) {
+    gpu_check(hipMemsetAsync(fctrl_->data(), 0, dev::kFusedCtrlWords * sizeof(unsigned), stream_),
+              "hipMemsetAsync");
+    dev::launch_yx_backward<T>(fargs_, fusedGrid_,
+                               static_cast<const cx<T>*>(grid_->device_slot(GridImpl<T>::kStickSide)),
+                               static_cast<cx<T>*>(space), fscratch_->data<cx<T>>(),
+                               twY_->data<cx<T>>(), twX_->data<cx<T>>(), stream_);
+    if (outputLocation == SPFFT_PU_HOST) {
+      gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
+                               hipMemcpyDeviceToHost, stream_),
+                "hipMemcpyAsync");
+    }
+    return;
+  }
   // plane chunks: the intermediate of a chunk is read back by the x stage while
   // it is still resident in the last-level (Infinity) cache
   const int L = plan_->local_planes();
@@ -528,6 +623,15 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
               "hipMemcpyAsync");
   }
   poison(false);
+  if (fused_) {
+    gpu_check(hipMemsetAsync(fctrl_->data(), 0, dev::kFusedCtrlWords * sizeof(unsigned), stream_),
+              "hipMemsetAsync");
+    dev::launch_xy_forward<T>(fargs_, fusedGrid_, static_cast<const cx<T>*>(space),
+                              static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kStickSide)),
+                              fscratch_->data<cx<T>>(), twY_->data<cx<T>>(), twX_->data<cx<T>>(),
+                              stream_);
+    return;
+  }
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides
@@ -594,6 +698,16 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   if (hostOut) values = staging(p.numLocalElements);
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kStickSide);
+  if (fused_) {
+    dev::launch_z_forward_pm<T>(fargs_, static_cast<const cx<T>*>(stick), values, factor,
+                                twZ_->data<cx<T>>(), stream_);
+    if (hostOut) {
+      gpu_check(hipMemcpyAsync(output, values, sizeof(cx<T>) * p.numLocalElements,
+                               hipMemcpyDeviceToHost, stream_),
+                "hipMemcpyAsync");
+    }
+    return;
+  }
   const auto a = zargs();
   if (floatExchange_)
     dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,

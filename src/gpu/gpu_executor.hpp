@@ -11,6 +11,7 @@
 
 #include "api/grid_impl.hpp"
 #include "gpu/gpu_runtime.hpp"
+#include "kernels/fused_stage.hpp"
 #include "kernels/stage_args.hpp"
 #include "plan/index_plan.hpp"
 
@@ -78,6 +79,16 @@ private:
   // hold those destinations as element offsets from the local buffer.
   bool peerWrites_ = false;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
+
+  // Fused single-GPU path (P = 1, C2C): plane-major sticks and the persistent
+  // XCD-cooperative y/x kernels (kernels/fused_stage.hip). Opt-in: SPFFT_FUSED=1.
+  bool fused_ = false;
+  int fusedGrid_ = 0;
+  dev::FusedArgs fargs_{};
+  std::unique_ptr<DeviceBuffer> entryCol_, fscratch_, fctrl_;
+  unsigned* fusedFailHost_ = nullptr;
+  void setup_fused();
+  void check_fused();
 
   // Pipelined exchange (RCCL / loopback data planes): the z stage (backward) and
   // the y stage (forward) run in K chunks of sticks / columns; chunk k's
