@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -111,6 +112,31 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     chunks = all[0];
     if (!peerWrites_ && chunkPlanes_ == 0 && chunks > 1) build_chunk_plan(chunks);
   }
+  log_plan();
+}
+
+// SPFFT_LOG=1: one line per transform with the plan decisions (engines, layout,
+// data plane, pipelining, fused path)
+template <typename T>
+void GpuExecutor<T>::log_plan() const {
+  const char* env = std::getenv("SPFFT_LOG");
+  if (!env || !*env || env[0] == '0') return;
+  const IndexPlan& p = *plan_;
+  const bool dbl = sizeof(T) == 8;
+  std::string plane = "none";
+  if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().kind();
+  std::fprintf(stderr,
+               "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
+               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d peer_writes=%d fused=%d\n",
+               p.rank, p.size, p.dimX, p.dimY, p.dimZ,
+               p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
+               p.local_planes(), p.num_columns(),
+               dev::describe_engine(p.dimZ, dbl, false).c_str(),
+               dev::describe_engine(p.dimY, dbl, true).c_str(),
+               dev::describe_engine(twXh_ ? p.dimX / 2 : p.dimX, dbl, true).c_str(),
+               twXh_ ? " packed-real" : "", layout_.buffered ? "buffered" : "compact",
+               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, peerWrites_ ? 1 : 0,
+               fused_ ? 1 : 0);
 }
 
 template <typename T>

@@ -49,6 +49,7 @@ private:
   void build_chunk_plan(int chunks);
   void pipelined_exchange(bool backward);
   void wait_stream();
+  void log_plan() const;
   void poison(bool backward);
   dev::ZArgs zargs() const;
   dev::YArgs yargs() const;

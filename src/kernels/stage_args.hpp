@@ -13,6 +13,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <string>
 
 #include "fft/codelets.hpp"
 #include "plan/index_plan.hpp"
@@ -62,6 +63,9 @@ struct XArgs {
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
   const int* colX;
 };
+
+// Engine geometry for diagnostics (SPFFT_LOG).
+std::string describe_engine(int n, bool dbl, bool lineFast);
 
 // Host launchers. `tw` is the length-n twiddle table exp(-2 pi i m / n).
 // BT is the exchange element type (cx<T> or cx<float> for *_FLOAT exchanges).

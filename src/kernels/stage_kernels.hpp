@@ -16,12 +16,6 @@ namespace dev {
 #ifndef SPFFT_ROW_STAGE
 #define SPFFT_ROW_STAGE 1
 #endif
-#ifndef SPFFT_XB_DIRECT
-#define SPFFT_XB_DIRECT 0
-#endif
-#ifndef SPFFT_YB_DIRECT
-#define SPFFT_YB_DIRECT 0
-#endif
 
 #ifndef SPFFT_NT
 #define SPFFT_NT 1
@@ -555,22 +549,11 @@ __global__ void __launch_bounds__(kMaxThreads)
   __syncthreads();
   const int zl = min(B, a.L - z0);
   if (c != a.colOfX0) {
-#if SPFFT_YB_DIRECT
-    eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
-      const int e = yEnt[pos];
-      if (e < 0 || b >= zl) return czero<T>();
-      return cvt<T>(ld_stream(&in[cBase[e] + b]));
-    }, [&](int b, int pos, cx<T> v) {
-      if (b < zl) st_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], v);
-    });
-    return;
-#else
     eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
       const int e = yEnt[pos];
       if (e < 0 || b >= zl) return czero<T>();
       return cvt<T>(ld_stream(&in[cBase[e] + b]));
     });
-#endif
   } else {
     zero_lds(lds, eng.input_elems());
     __syncthreads();
@@ -664,16 +647,6 @@ __global__ void __launch_bounds__(kMaxThreads)
     return c < 0 ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
-#if SPFFT_XB_DIRECT
-  // line-fast lanes store rows directly: a wave writes B rows x (64/B) consecutive x
-  eng.global_to_global(lds, tw, load, [&](int b, int pos, cx<T> v) {
-    if (b >= yl) return;
-    if (R2C)
-      st_stream_real(&static_cast<T*>(space)[row0 + static_cast<long long>(b) * n + pos], v.x);
-    else
-      st_stream(&static_cast<cx<T>*>(space)[row0 + static_cast<long long>(b) * n + pos], v);
-  });
-#else
   eng.global_to_lds(lds, tw, load);
   for (int idx = threadIdx.x; idx < yl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
@@ -682,7 +655,6 @@ __global__ void __launch_bounds__(kMaxThreads)
     else
       st_stream(&static_cast<cx<T>*>(space)[row0 + idx], lds[eng.out_at(b, pos)]);
   }
-#endif
 }
 
 // Forward x stage, line-fast engine: lanes read row segments of the space

@@ -1,4 +1,6 @@
 // x-stage launchers: [z][column][y] <-> space domain rows (C2C, C2R, R2C).
+#include <string>
+
 #include "kernels/stage_kernels.hpp"
 
 namespace spfft {
@@ -80,6 +82,23 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
   if (lines < 1) lines = 1;
   p.lines = lines;
   return p;
+}
+
+std::string describe_engine(int n, bool dbl, bool lineFast) {
+  std::string out;
+  auto fmt = [&](auto eng, int threads, int lines, std::size_t lds) {
+    (void)eng;
+    out = "n=" + std::to_string(n) + " lines=" + std::to_string(lines) + " threads=" +
+          std::to_string(threads) + " lds=" + std::to_string(lds);
+  };
+  if (dbl) {
+    if (lineFast) with_engine<double, +1, true>(n, fmt);
+    else with_engine<double, +1, false>(n, fmt);
+  } else {
+    if (lineFast) with_engine<float, +1, true>(n, fmt);
+    else with_engine<float, +1, false>(n, fmt);
+  }
+  return (has_ct_kernel(n) ? "ct " : "rt ") + out;
 }
 
 int max_device_fft_length(bool dbl) { return (160 * 1024) / (2 * (dbl ? 16 : 8)) - 1; }
