@@ -63,7 +63,7 @@ void HostExecutor<T>::z_backward(const cx<T>* values, BT* stick) {
   const int Z = p.dimZ;
   const bool r2c = p.type == SPFFT_TRANS_R2C;
   grid_->pool().parallel_for(p.local_sticks(), 16, [&](i64 b, i64 e, int t) {
-    cx<T>* buf = scratch(t, 3 * static_cast<std::size_t>(Z));
+    cx<T>* buf = scratch(t, static_cast<std::size_t>(Z) + fftZ_.scratch_size());
     cx<T>* fs = buf + Z;
     for (i64 s = b; s < e; ++s) {
       std::fill(buf, buf + Z, mk<T>(T(0), T(0)));
@@ -89,7 +89,7 @@ void HostExecutor<T>::y_backward(const BT* slab, cx<T>* inter) {
   const int Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   const bool r2c = p.type == SPFFT_TRANS_R2C;
   grid_->pool().parallel_for(static_cast<i64>(C) * L, std::max(1, L / 4), [&](i64 b, i64 e, int t) {
-    cx<T>* col = scratch(t, 3 * static_cast<std::size_t>(Y));
+    cx<T>* col = scratch(t, static_cast<std::size_t>(Y) + fftY_.scratch_size());
     cx<T>* fs = col + Y;
     for (i64 task = b; task < e; ++task) {
       const int c = static_cast<int>(task / L), zl = static_cast<int>(task % L);
@@ -108,7 +108,7 @@ void HostExecutor<T>::x_backward(const cx<T>* inter, T* space) {
   const int X = p.dimX, Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   const bool r2c = p.type == SPFFT_TRANS_R2C;
   grid_->pool().parallel_for(static_cast<i64>(L) * Y, 16, [&](i64 b, i64 e, int t) {
-    cx<T>* row = scratch(t, 3 * static_cast<std::size_t>(X));
+    cx<T>* row = scratch(t, static_cast<std::size_t>(X) + fftX_.scratch_size());
     cx<T>* fs = row + X;
     for (i64 rIdx = b; rIdx < e; ++rIdx) {
       const i64 zl = rIdx / Y, y = rIdx % Y;
@@ -133,7 +133,7 @@ void HostExecutor<T>::x_forward(const T* space, cx<T>* inter) {
   const int X = p.dimX, Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   const bool r2c = p.type == SPFFT_TRANS_R2C;
   grid_->pool().parallel_for(static_cast<i64>(L) * Y, 16, [&](i64 b, i64 e, int t) {
-    cx<T>* row = scratch(t, 3 * static_cast<std::size_t>(X));
+    cx<T>* row = scratch(t, static_cast<std::size_t>(X) + fftX_.scratch_size());
     cx<T>* fs = row + X;
     for (i64 rIdx = b; rIdx < e; ++rIdx) {
       const i64 zl = rIdx / Y, y = rIdx % Y;
@@ -155,7 +155,7 @@ void HostExecutor<T>::y_forward(const cx<T>* inter, BT* slab) {
   const IndexPlan& p = *plan_;
   const int Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   grid_->pool().parallel_for(static_cast<i64>(C) * L, std::max(1, L / 4), [&](i64 b, i64 e, int t) {
-    cx<T>* col = scratch(t, 3 * static_cast<std::size_t>(Y));
+    cx<T>* col = scratch(t, static_cast<std::size_t>(Y) + fftY_.scratch_size());
     cx<T>* fs = col + Y;
     for (i64 task = b; task < e; ++task) {
       const int c = static_cast<int>(task / L), zl = static_cast<int>(task % L);
@@ -172,7 +172,7 @@ void HostExecutor<T>::z_forward(const BT* stick, cx<T>* values, T factor) {
   const IndexPlan& p = *plan_;
   const int Z = p.dimZ;
   grid_->pool().parallel_for(p.local_sticks(), 16, [&](i64 b, i64 e, int t) {
-    cx<T>* buf = scratch(t, 3 * static_cast<std::size_t>(Z));
+    cx<T>* buf = scratch(t, static_cast<std::size_t>(Z) + fftZ_.scratch_size());
     cx<T>* fs = buf + Z;
     for (i64 s = b; s < e; ++s) {
       for (int r = 0; r < p.size; ++r) {

@@ -362,8 +362,12 @@ struct FftRT {
   // Input in region 0 at in_at(b, pos); returns the region holding the result
   // (index b*ls + pos). Ends with a barrier.
   __device__ static cx<T>* run_in_lds(const RtPlan& p, cx<T>* lds, const cx<T>* __restrict__ tw) {
-    cx<T>* src = lds;
-    cx<T>* dst = lds + p.lines * p.ls;
+    return run_between(p, lds, lds + p.lines * p.ls, tw);
+  }
+
+  // Ping-pong between two LDS regions (input in src); returns the result region.
+  __device__ static cx<T>* run_between(const RtPlan& p, cx<T>* src, cx<T>* dst,
+                                       const cx<T>* __restrict__ tw) {
     int ns = 1;
     for (int i = 0; i < p.np; ++i) {
       const int R = p.radix[i];

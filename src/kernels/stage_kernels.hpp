@@ -161,6 +161,78 @@ struct RtEng {
   }
 };
 
+// Bluestein engine for lengths with a large prime factor (chirp-z: one
+// convolution of power-of-two length m >= 2n-1 done with two run-time FFTs in
+// LDS). X_k = d_k sum_j (x_j d_j) conj(d_{k-j}), d_j = exp(S i pi j^2 / n).
+// Tables (device, per length): chirp d (S = -1) [n], FFT_m of the conj(d)
+// filter for S = -1 and S = +1 [2m], twiddles of length m [m].
+template <typename T, int S>
+struct BlueEng {
+  RtPlan pm;  // length m, ls = m
+  int nn;
+  const cx<T>* chirp;
+  const cx<T>* filt;
+  const cx<T>* twm;
+  __device__ int lines() const { return pm.lines; }
+  __device__ int n() const { return nn; }
+  __device__ int in_at(int b, int pos) const { return b * pm.ls + pos; }
+  __device__ int out_at(int b, int pos) const { return b * pm.ls + pos; }
+  __device__ int input_elems() const { return pm.lines * pm.ls; }
+  __device__ int lds_bytes() const { return 2 * pm.lines * pm.ls * static_cast<int>(sizeof(cx<T>)); }
+  __device__ cx<T> d(int j) const { return S < 0 ? chirp[j] : conj(chirp[j]); }
+  __device__ void run(cx<T>* lds) const {
+    const int m = pm.n, total = pm.lines * m;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int b = idx / m, j = idx - b * m;
+      cx<T>& v = lds[b * pm.ls + j];
+      v = j < nn ? cmul(v, d(j)) : mk<T>(T(0), T(0));
+    }
+    __syncthreads();
+    cx<T>* A = lds;
+    cx<T>* B = lds + pm.lines * pm.ls;
+    cx<T>* r = FftRT<T, -1>::run_between(pm, A, B, twm);
+    const cx<T>* f = filt + (S < 0 ? 0 : m);
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int b = idx / m, j = idx - b * m;
+      r[b * pm.ls + j] = cmul(r[b * pm.ls + j], f[j]);
+    }
+    __syncthreads();
+    cx<T>* r2 = FftRT<T, +1>::run_between(pm, r, r == A ? B : A, twm);
+    const T inv = T(1) / static_cast<T>(m);
+    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
+      const int b = idx / nn, k = idx - b * nn;
+      A[b * pm.ls + k] = scale(cmul(r2[b * pm.ls + k], d(k)), inv);
+    }
+    __syncthreads();
+  }
+  template <class St>
+  __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__, St st) const {
+    run(lds);
+    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
+      const int b = idx / nn, k = idx - b * nn;
+      st(b, k, lds[out_at(b, k)]);
+    }
+  }
+  template <class Ld>
+  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
+    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
+      const int b = idx / nn, k = idx - b * nn;
+      lds[in_at(b, k)] = ld(b, k);
+    }
+    __syncthreads();
+    run(lds);
+  }
+  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__) const { run(lds); }
+  template <class Ld, class St>
+  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+    global_to_lds(lds, tw, ld);
+    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
+      const int b = idx / nn, k = idx - b * nn;
+      st(b, k, lds[out_at(b, k)]);
+    }
+  }
+};
+
 template <typename To, typename From>
 __device__ __forceinline__ cx<To> cvt(const cx<From>& v) {
   return mk<To>(static_cast<To>(v.x), static_cast<To>(v.y));
@@ -797,6 +869,17 @@ __global__ void __launch_bounds__(kMaxThreads)
 // ------------------------------------------------------------ host helpers
 RtPlan make_rt_plan(int n, std::size_t elemBytes);
 
+// Bluestein plan and device tables of length n (cached per device), or
+// nullptr-tables when n does not use Bluestein.
+struct BlueTables {
+  RtPlan pm;
+  const void* chirp = nullptr;
+  const void* filt = nullptr;
+  const void* twm = nullptr;
+};
+bool use_bluestein(int n, std::size_t elemBytes);
+BlueTables bluestein_tables(int n, bool dbl);
+
 template <class K>
 inline void prepare_kernel(K kernel, std::size_t ldsBytes) {
   if (ldsBytes > 64 * 1024) {
@@ -827,6 +910,13 @@ inline void with_engine(int n, F&& f) {
     SPFFT_CT_CASE(1024)
 #undef SPFFT_CT_CASE
     default: {
+      if (use_bluestein(n, sizeof(cx<T>))) {
+        const BlueTables bt = bluestein_tables(n, sizeof(T) == 8);
+        BlueEng<T, S> e{bt.pm, n, static_cast<const cx<T>*>(bt.chirp),
+                        static_cast<const cx<T>*>(bt.filt), static_cast<const cx<T>*>(bt.twm)};
+        f(e, kMaxThreads, e.pm.lines, std::size_t(2) * e.pm.lines * e.pm.ls * sizeof(cx<T>));
+        return;
+      }
       RtEng<T, S> e{make_rt_plan(n, sizeof(cx<T>))};
       f(e, kMaxThreads, e.p.lines, std::size_t(2) * e.p.lines * e.p.ls * sizeof(cx<T>));
       return;

@@ -1,7 +1,13 @@
 // x-stage launchers: [z][column][y] <-> space domain rows (C2C, C2R, R2C).
 #include <string>
+#include <vector>
+#include <tuple>
+#include <mutex>
+#include <map>
 
 #include "kernels/stage_kernels.hpp"
+// after the HIP headers (codelets use __forceinline__ under hipcc)
+#include "fft/host_fft.hpp"
 
 namespace spfft {
 namespace dev {
@@ -99,6 +105,93 @@ std::string describe_engine(int n, bool dbl, bool lineFast) {
     else with_engine<float, +1, false>(n, fmt);
   }
   return (has_ct_kernel(n) ? "ct " : "rt ") + out;
+}
+
+// ------------------------------------------------------------- Bluestein
+bool use_bluestein(int n, std::size_t elemBytes) {
+  if (n < 2 || has_ct_kernel(n)) return false;
+  const std::vector<int> r = factorize_radices(n);
+  if (r.empty() || r.back() <= kBluesteinPrime) return false;
+  int m = 1;
+  while (m < 2 * n - 1) m *= 2;
+  return 2 * static_cast<std::size_t>(m) * elemBytes <= 160 * 1024;
+}
+
+namespace {
+template <typename T>
+void fill_bluestein(int n, int m, std::vector<cx<T>>& chirp, std::vector<cx<T>>& filt,
+                    std::vector<cx<T>>& tw) {
+  const long double pi = 3.141592653589793238462643383279502884L;
+  chirp.resize(n);
+  for (int j = 0; j < n; ++j) {
+    const long long q = (static_cast<long long>(j) * j) % (2LL * n);
+    const long double a = pi * static_cast<long double>(q) / static_cast<long double>(n);
+    chirp[j] = mk<T>(static_cast<T>(std::cos(a)), static_cast<T>(-std::sin(a)));
+  }
+  // filters: FFT_m of b (b_j = conj(d_j), b_{m-j} = conj(d_j)), computed on the host
+  // in long double precision via the host engine in double
+  HostFft<double> fft(m);
+  std::vector<cx<double>> work(fft.scratch_size()), b(m);
+  filt.resize(2 * static_cast<std::size_t>(m));
+  for (int s = 0; s < 2; ++s) {
+    for (auto& v : b) v = mk<double>(0.0, 0.0);
+    for (int j = 0; j < n; ++j) {
+      const long long q = (static_cast<long long>(j) * j) % (2LL * n);
+      const long double a = pi * static_cast<long double>(q) / static_cast<long double>(n);
+      // conj(d_j) with d_j = exp(S i a): S = -1 -> exp(+i a), S = +1 -> exp(-i a)
+      const cx<double> c = mk<double>(static_cast<double>(std::cos(a)),
+                                      static_cast<double>(s == 0 ? std::sin(a) : -std::sin(a)));
+      b[j] = c;
+      if (j > 0) b[m - j] = c;
+    }
+    fft.execute(b.data(), 1, b.data(), 1, -1, work.data());
+    for (int j = 0; j < m; ++j)
+      filt[static_cast<std::size_t>(s) * m + j] = mk<T>(static_cast<T>(b[j].x), static_cast<T>(b[j].y));
+  }
+  tw = make_twiddles<T>(m);
+}
+}  // namespace
+
+BlueTables bluestein_tables(int n, bool dbl) {
+  static std::mutex mutex;
+  static std::map<std::tuple<int, int, bool>, std::pair<BlueTables, DeviceBuffer*>> cache;
+  int device = 0;
+  gpu_check(hipGetDevice(&device), "hipGetDevice");
+  std::lock_guard<std::mutex> lock(mutex);
+  auto it = cache.find(std::make_tuple(device, n, dbl));
+  if (it != cache.end()) return it->second.first;
+  int m = 1;
+  while (m < 2 * n - 1) m *= 2;
+  const std::size_t eb = dbl ? sizeof(cx<double>) : sizeof(cx<float>);
+  BlueTables t;
+  t.pm = make_rt_plan(m, eb);
+  t.pm.ls = m;
+  t.pm.lines = std::max<std::size_t>(1, kLdsBudget / (2 * static_cast<std::size_t>(m) * eb));
+  if (t.pm.lines > 16) t.pm.lines = 16;
+  // one allocation: chirp [n] | filters [2m] | twiddles [m]; lives for the process
+  auto* buf = new DeviceBuffer((static_cast<std::size_t>(n) + 3 * static_cast<std::size_t>(m)) * eb);
+  auto upload = [&](auto& chirp, auto& filt, auto& tw) {
+    char* base = buf->data<char>();
+    gpu_check(hipMemcpy(base, chirp.data(), n * eb, hipMemcpyHostToDevice), "hipMemcpy");
+    gpu_check(hipMemcpy(base + n * eb, filt.data(), 2 * m * eb, hipMemcpyHostToDevice), "hipMemcpy");
+    gpu_check(hipMemcpy(base + (n + 2 * static_cast<std::size_t>(m)) * eb, tw.data(), m * eb,
+                        hipMemcpyHostToDevice),
+              "hipMemcpy");
+    t.chirp = base;
+    t.filt = base + n * eb;
+    t.twm = base + (n + 2 * static_cast<std::size_t>(m)) * eb;
+  };
+  if (dbl) {
+    std::vector<cx<double>> c, f, w;
+    fill_bluestein<double>(n, m, c, f, w);
+    upload(c, f, w);
+  } else {
+    std::vector<cx<float>> c, f, w;
+    fill_bluestein<float>(n, m, c, f, w);
+    upload(c, f, w);
+  }
+  cache.emplace(std::make_tuple(device, n, dbl), std::make_pair(t, buf));
+  return t;
 }
 
 int max_device_fft_length(bool dbl) { return (160 * 1024) / (2 * (dbl ? 16 : 8)) - 1; }

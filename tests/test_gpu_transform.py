@@ -352,3 +352,30 @@ def test_fused_xcd_path(gpu, n, monkeypatch):
         assert ((out - ref).abs().max() / ref.abs().max()).item() < 1e-12
         f = t.forward(None, scaling=sp.Scaling.FULL)
         assert ((f - vals).abs().max() / vals.abs().max()).item() < 1e-12
+
+
+@pytest.mark.parametrize("dims,r2c,single", [((67, 8, 101), False, False), ((127, 3, 2), False, False),
+                                             ((103, 16, 67), True, False), ((2, 257, 5), False, True),
+                                             ((1021, 2, 3), False, False), ((97, 89, 4), True, True)])
+def test_gpu_bluestein(gpu, dims, r2c, single):
+    """GPU lengths with a prime factor > 61: Bluestein engine (chirp-z, power-of-two
+    convolution in LDS) inside the stage kernels."""
+    import torch
+    nx, ny, nz = dims
+    rng = np.random.default_rng(31)
+    idx = create_value_indices(rng, [1.0], 0.8, 0.9, nx, ny, nz, r2c)[0]
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    vals = dense_forward(space, idx, dims, r2c=r2c)
+    tol = 2e-5 if single else 1e-11
+    cls = sp.GridFloat if single else sp.Grid
+    g = cls(nx, ny, nz, nx * ny, GPU, 1)
+    t = g.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                           nx, ny, nz, nz, idx)
+    vdt = np.complex64 if single else np.complex128
+    out = t.backward(torch.as_tensor(vals.astype(vdt), device=gpu))
+    assert max_rel_error(out.cpu().numpy(), dense_backward(idx, vals, dims, r2c=r2c)) < tol
+    sdt = (np.float32 if r2c else np.complex64) if single else space.dtype
+    f = t.forward(torch.as_tensor(space.astype(sdt), device=gpu))
+    assert max_rel_error(f.cpu().numpy(), vals) < tol

@@ -85,3 +85,23 @@ def test_single_precision_host():
     out = t.backward(vals)
     assert out.dtype == np.complex64
     assert max_rel_error(out, dense_backward(idx, vals, dims)) < 1e-5
+
+
+@pytest.mark.parametrize("dims", [(67, 3, 2), (101, 103, 4), (127, 2, 131), (2, 257, 3), (199, 1, 1)])
+@pytest.mark.parametrize("r2c", [False, True])
+def test_large_prime_bluestein(dims, r2c):
+    """Lengths with a prime factor > 61 run through Bluestein's algorithm (host)."""
+    nx, ny, nz = dims
+    rng = np.random.default_rng(3)
+    idx = create_value_indices(rng, [1.0], 0.8, 0.9, nx, ny, nz, r2c)[0]
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    vals = dense_forward(space, idx, dims, r2c=r2c)
+    g = sp.Grid(nx, ny, nz, nx * ny, sp.ProcessingUnit.HOST, 2)
+    t = g.create_transform(sp.ProcessingUnit.HOST, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                           nx, ny, nz, nz, idx)
+    out = np.array(t.backward(vals))
+    assert max_rel_error(out, dense_backward(idx, vals, dims, r2c=r2c)) < 1e-12
+    f = np.array(t.forward(space))
+    assert max_rel_error(f, vals) < 1e-12
