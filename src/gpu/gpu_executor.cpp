@@ -45,6 +45,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
   chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
+  interRing_ = chunkPlanes_ > 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
+  interRing_ = chunkPlanes_ > 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
@@ -592,7 +594,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
     throw InvalidParameterError();
   DeviceGuard guard(deviceId_);
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
-  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  auto* interBase = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
   if (fused_) {
@@ -618,6 +620,9 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
     auto xa = xargs();
     ya.zBegin = xa.zBegin = zb;
     ya.L = xa.L = std::min(L, zb + chunk);
+    // ring mode: every chunk reuses the first `chunk` planes of the intermediate
+    cx<T>* inter =
+        interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (floatExchange_)
       dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
                                            twY_->data<cx<T>>(), stream_);
@@ -658,7 +663,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
                               stream_);
     return;
   }
-  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  auto* interBase = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides
   if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
@@ -669,6 +674,8 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     auto xa = xargs();
     ya.zBegin = xa.zBegin = zb;
     ya.L = xa.L = std::min(L, zb + chunk);
+    cx<T>* inter =
+        interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (peerWrites_) {
       ya.colBase = colBaseRemote_->data<long long>();
       ya.remote = 1;

@@ -63,6 +63,7 @@ private:
   bool floatExchange_ = false;
   long long interStride_ = 0;  // row stride of [z][column][y]
   int chunkPlanes_ = 0;        // y/x stages interleaved per chunk of planes (0 = off)
+  bool interRing_ = false;     // plane chunks share one chunk-sized intermediate (cache-resident)
   bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;
 

@@ -304,7 +304,8 @@ struct RtPlan {
   int n;       // length
   int np;      // number of passes
   int ls;      // line stride (elements)
-  int lines;   // lines per block
+  int lines;   // lines per block (a power of two)
+  int linesLog2;
   int radix[16];
 };
 

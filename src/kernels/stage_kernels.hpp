@@ -49,6 +49,28 @@ __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
   *p = v;
 #endif
 }
+// The [z][column][y] intermediate: streamed like the rest by default; with
+// SPFFT_NT_INTER=0 it keeps the default cache policy (plane-chunked ring mode,
+// where the x stage re-reads a chunk while it is resident in the Infinity Cache).
+#ifndef SPFFT_NT_INTER
+#define SPFFT_NT_INTER SPFFT_NT
+#endif
+template <typename T>
+__device__ __forceinline__ cx<T> ld_inter(const cx<T>* p) {
+#if SPFFT_NT_INTER
+  return ld_stream(p);
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_inter(cx<T>* p, cx<T> v) {
+#if SPFFT_NT_INTER
+  st_stream(p, v);
+#else
+  *p = v;
+#endif
+}
 // Sparse frequency values: a stick's values rarely start on a cache-line
 // boundary, so neighbouring workgroups share lines; plain accesses keep them.
 template <typename T>
@@ -115,7 +137,11 @@ struct CtEng {
   static std::size_t h_lds() { return F::lds_bytes(); }
 };
 
-template <typename T, int S>
+// Run-time length engine. LF (line-fast) engines walk the global side with the
+// line index fastest — consecutive lanes touch consecutive lines, i.e. the
+// contiguous z-run of a stick or y-run of an intermediate column — like the
+// compile-time line-fast mapping; row engines walk positions fastest.
+template <typename T, int S, bool LF = false>
 struct RtEng {
   RtPlan p;
   __device__ int lines() const { return p.lines; }
@@ -128,12 +154,24 @@ struct RtEng {
   __device__ int lds_bytes() const {
     return 2 * p.lines * p.ls * static_cast<int>(sizeof(cx<T>));
   }
+  // global-side element idx -> (line b, position pos); plan lines are a power
+  // of two (make_rt_plan), so the line-fast split is a mask and a shift
+  __device__ void split(int idx, int& b, int& pos) const {
+    if (LF) {
+      b = idx & (p.lines - 1);
+      pos = idx >> p.linesLog2;
+    } else {
+      b = idx / p.n;
+      pos = idx - b * p.n;
+    }
+  }
   template <class St>
   __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     const cx<T>* res = FftRT<T, S>::run_in_lds(p, lds, tw);
     const int total = p.lines * p.n;
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-      const int b = idx / p.n, pos = idx - b * p.n;
+      int b, pos;
+      split(idx, b, pos);
       st(b, pos, res[b * p.ls + pos]);
     }
   }
@@ -141,7 +179,8 @@ struct RtEng {
   __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
     const int total = p.lines * p.n;
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-      const int b = idx / p.n, pos = idx - b * p.n;
+      int b, pos;
+      split(idx, b, pos);
       lds[b * p.ls + pos] = ld(b, pos);
     }
     __syncthreads();
@@ -155,7 +194,8 @@ struct RtEng {
     global_to_lds(lds, tw, ld);
     const int total = p.lines * p.n;
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-      const int b = idx / p.n, pos = idx - b * p.n;
+      int b, pos;
+      split(idx, b, pos);
       st(b, pos, lds[out_at(b, pos)]);
     }
   }
@@ -643,7 +683,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   // rows of [z][column][y] are contiguous: coalesced copy-out
   for (int idx = threadIdx.x; idx < zl * n; idx += blockDim.x) {
     const int b = idx / n, pos = idx - b * n;
-    st_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], lds[eng.out_at(b, pos)]);
+    st_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], lds[eng.out_at(b, pos)]);
   }
 }
 
@@ -673,7 +713,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   const int zl = min(B, a.L - z0);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return ld_stream(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
+    return ld_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const int e = yEnt[pos];
@@ -713,10 +753,10 @@ __global__ void __launch_bounds__(kMaxThreads)
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xCol[n - pos];
-      return c < 0 ? czero<T>() : conj(ld_stream(&src[static_cast<long long>(c) * a.interStride + b]));
+      return c < 0 ? czero<T>() : conj(ld_inter(&src[static_cast<long long>(c) * a.interStride + b]));
     }
     const int c = xCol[pos];
-    return c < 0 ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+    return c < 0 ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
@@ -756,7 +796,7 @@ __global__ void __launch_bounds__(kMaxThreads)
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const int c = xCol[pos];
-    if (c >= 0 && b < yl) st_stream(&dst[static_cast<long long>(c) * a.interStride + b], v);
+    if (c >= 0 && b < yl) st_inter(&dst[static_cast<long long>(c) * a.interStride + b], v);
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
@@ -799,14 +839,14 @@ __global__ void __launch_bounds__(kMaxThreads)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
     const int k = idx / B, b = idx - k * B;
     const int c = xCol[k];
-    return (c < 0 || b >= yl) ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   }, [&](int idx) {
     const int k = idx / B;
     return eng.in_at(idx - k * B, k);
   });
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int c = xCol[h];
-    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_stream(&src[static_cast<long long>(c) * a.interStride + b]);
+    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   }
   __syncthreads();
   // pre-pass in place, pairs (k, h-k): Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k
@@ -862,7 +902,7 @@ __global__ void __launch_bounds__(kMaxThreads)
     const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
     const cx<T> e = scale(yk + ym, T(0.5));
     const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
-    st_stream(&dst[static_cast<long long>(c) * a.interStride + b], e + twm<-1>(o, twn[k]));
+    st_inter(&dst[static_cast<long long>(c) * a.interStride + b], e + twm<-1>(o, twn[k]));
   }
 }
 
@@ -917,7 +957,7 @@ inline void with_engine(int n, F&& f) {
         f(e, kMaxThreads, e.pm.lines, std::size_t(2) * e.pm.lines * e.pm.ls * sizeof(cx<T>));
         return;
       }
-      RtEng<T, S> e{make_rt_plan(n, sizeof(cx<T>))};
+      RtEng<T, S, LF> e{make_rt_plan(n, sizeof(cx<T>))};
       f(e, kMaxThreads, e.p.lines, std::size_t(2) * e.p.lines * e.p.ls * sizeof(cx<T>));
       return;
     }

@@ -85,8 +85,10 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
   if (line > 160 * 1024) throw GPUFFTError();
   int lines = static_cast<int>(kLdsBudget / line);
   if (lines > kMaxThreads) lines = kMaxThreads;
-  if (lines < 1) lines = 1;
-  p.lines = lines;
+  // a power of two: line-fast engines split lane indices with shifts
+  p.linesLog2 = 0;
+  while ((2 << p.linesLog2) <= lines) ++p.linesLog2;
+  p.lines = 1 << p.linesLog2;
   return p;
 }
 
