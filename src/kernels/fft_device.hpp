@@ -7,8 +7,12 @@
 //    one element per 256-byte bank row, and consecutive lines start 16 bytes
 //    apart in the bank space, so both the strided pass writes and the
 //    column-wise gathers of the stage kernels are bank-conflict free.
-//  FftRT<T, S>: run-time length (any N, mixed radix incl. generic primes),
-//    ping-pong Stockham entirely in LDS. Used for lengths without a CT shape.
+//  FftRT<T, S>: run-time length (any N, mixed radix incl. generic primes).
+//    Lengths whose radices all have codelets run in place: each pass stages
+//    the lane's butterflies in VGPRs between two barriers, work items lines
+//    fastest, divisions by precomputed reciprocals. Lengths with a generic
+//    prime pass ping-pong between two LDS regions. Used for lengths without
+//    a CT shape.
 //
 // Sign S = +1 is the backward (frequency -> space) direction.
 #pragma once
@@ -31,6 +35,14 @@ constexpr int kMaxThreads = 256;
 #endif
 // LDS per workgroup for the FFT lines (tuning knob; see tools/gpu_variants.sh)
 constexpr int kLdsBudget = SPFFT_LDS_BUDGET;
+// Elements per workgroup of the in-place run-time engine (lines * n): it bounds
+// the lanes' register staging (lines * n / (R * threads) butterflies per pass).
+// 4096 = 64 KB of complex<double>, 32 KB of complex<float>: the best of the
+// 32/64 KB budgets measured for each precision (profiles/README.md, session 5).
+#ifndef SPFFT_RT_ELEMS
+#define SPFFT_RT_ELEMS 4096
+#endif
+constexpr int kRtElems = SPFFT_RT_ELEMS;
 
 template <typename T>
 struct LdsGeom;
@@ -306,12 +318,87 @@ struct RtPlan {
   int ls;      // line stride (elements)
   int lines;   // lines per block (a power of two)
   int linesLog2;
+  int inplace;          // 1: every radix has a codelet -> one LDS region, register-staged passes
+  unsigned nMagic;      // ceil(2^32 / n): idx / n == umulhi(idx, nMagic) for idx * n < 2^32
   int radix[16];
+  unsigned nsMagic[16];  // ceil(2^32 / ns) of each pass (ns = product of the earlier radices)
 };
+
+// Radices with a codelet (the in-place run-time passes are instantiated for these).
+__host__ __device__ constexpr bool rt_codelet_radix(int r) {
+  return r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8 || r == 9 || r == 11 ||
+         r == 13 || r == 16;
+}
 
 template <typename T, int S>
 struct FftRT {
   __device__ static int in_at(const RtPlan& p, int b, int pos) { return b * p.ls + pos; }
+
+  // In-place Stockham pass of radix R over all lines of the block (blockDim.x ==
+  // kMaxThreads). Work item idx -> (line b = idx mod lines, butterfly j = idx /
+  // lines): lines fastest, so a wave's LDS accesses spread over the lines' bank
+  // offsets (plan stride, make_rt_plan). Every lane loads all its butterflies
+  // into registers before the barrier and stores after it.
+  template <int R>
+  __device__ static void pass_inplace(const RtPlan& p, cx<T>* buf, int ns, unsigned nsMagic,
+                                      const cx<T>* __restrict__ tw) {
+    constexpr int kElems = kRtElems;
+    constexpr int kIt = (kElems + R * kMaxThreads - 1) / (R * kMaxThreads);
+    const int nb = p.n / R;
+    const int total = nb << p.linesLog2;
+    const int twStride = p.n / (ns * R);
+    cx<T> v[kIt][R];
+    int dst[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = threadIdx.x + it * kMaxThreads;
+      if (idx < total) {
+        const int b = idx & (p.lines - 1);
+        const int j = idx >> p.linesLog2;
+        const int kk =
+            ns == 1 ? 0 : j - ns * static_cast<int>(__umulhi(static_cast<unsigned>(j), nsMagic));
+        const cx<T>* s = buf + b * p.ls + j;
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[it][r] = s[r * nb];
+        if (kk) {
+#pragma unroll
+          for (int r = 1; r < R; ++r) v[it][r] = twm<S>(v[it][r], tw[kk * r * twStride]);
+        }
+        Dft<R, S, T>::run(v[it]);
+        dst[it] = b * p.ls + (j - kk) * R + kk;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int idx = threadIdx.x + it * kMaxThreads;
+      if (idx < total) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[dst[it] + r * ns] = v[it][r];
+      }
+    }
+    __syncthreads();
+  }
+
+  __device__ static void run_inplace(const RtPlan& p, cx<T>* buf, const cx<T>* __restrict__ tw) {
+    int ns = 1;
+    for (int i = 0; i < p.np; ++i) {
+      const unsigned m = p.nsMagic[i];
+      switch (p.radix[i]) {
+        case 2: pass_inplace<2>(p, buf, ns, m, tw); break;
+        case 3: pass_inplace<3>(p, buf, ns, m, tw); break;
+        case 4: pass_inplace<4>(p, buf, ns, m, tw); break;
+        case 5: pass_inplace<5>(p, buf, ns, m, tw); break;
+        case 7: pass_inplace<7>(p, buf, ns, m, tw); break;
+        case 8: pass_inplace<8>(p, buf, ns, m, tw); break;
+        case 9: pass_inplace<9>(p, buf, ns, m, tw); break;
+        case 11: pass_inplace<11>(p, buf, ns, m, tw); break;
+        case 13: pass_inplace<13>(p, buf, ns, m, tw); break;
+        default: pass_inplace<16>(p, buf, ns, m, tw); break;
+      }
+      ns *= p.radix[i];
+    }
+  }
 
   template <int R>
   __device__ static void pass(const RtPlan& p, const cx<T>* src, cx<T>* dst, int ns,
@@ -363,6 +450,10 @@ struct FftRT {
   // Input in region 0 at in_at(b, pos); returns the region holding the result
   // (index b*ls + pos). Ends with a barrier.
   __device__ static cx<T>* run_in_lds(const RtPlan& p, cx<T>* lds, const cx<T>* __restrict__ tw) {
+    if (p.inplace) {
+      run_inplace(p, lds, tw);
+      return lds;
+    }
     return run_between(p, lds, lds + p.lines * p.ls, tw);
   }
 

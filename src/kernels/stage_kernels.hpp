@@ -148,20 +148,21 @@ struct RtEng {
   __device__ int n() const { return p.n; }
   __device__ int in_at(int b, int pos) const { return b * p.ls + pos; }
   __device__ int out_at(int b, int pos) const {
-    return ((p.np & 1) ? p.lines * p.ls : 0) + b * p.ls + pos;
+    return ((!p.inplace && (p.np & 1)) ? p.lines * p.ls : 0) + b * p.ls + pos;
   }
   __device__ int input_elems() const { return p.lines * p.ls; }
   __device__ int lds_bytes() const {
-    return 2 * p.lines * p.ls * static_cast<int>(sizeof(cx<T>));
+    return (p.inplace ? 1 : 2) * p.lines * p.ls * static_cast<int>(sizeof(cx<T>));
   }
   // global-side element idx -> (line b, position pos); plan lines are a power
-  // of two (make_rt_plan), so the line-fast split is a mask and a shift
+  // of two (make_rt_plan), so the line-fast split is a mask and a shift, and
+  // the row split divides by a precomputed reciprocal
   __device__ void split(int idx, int& b, int& pos) const {
     if (LF) {
       b = idx & (p.lines - 1);
       pos = idx >> p.linesLog2;
     } else {
-      b = idx / p.n;
+      b = p.n == 1 ? idx : static_cast<int>(__umulhi(static_cast<unsigned>(idx), p.nMagic));
       pos = idx - b * p.n;
     }
   }
@@ -958,7 +959,8 @@ inline void with_engine(int n, F&& f) {
         return;
       }
       RtEng<T, S, LF> e{make_rt_plan(n, sizeof(cx<T>))};
-      f(e, kMaxThreads, e.p.lines, std::size_t(2) * e.p.lines * e.p.ls * sizeof(cx<T>));
+      f(e, kMaxThreads, e.p.lines,
+        std::size_t(e.p.inplace ? 1 : 2) * e.p.lines * e.p.ls * sizeof(cx<T>));
       return;
     }
   }

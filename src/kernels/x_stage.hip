@@ -79,16 +79,45 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
   const std::vector<int> r = factorize_radices(n);
   if (r.size() > 16) throw GPUFFTError();
   p.np = static_cast<int>(r.size());
-  for (int i = 0; i < p.np; ++i) p.radix[i] = r[i];
-  p.ls = n + 1;
-  const std::size_t line = 2 * static_cast<std::size_t>(p.ls) * elemBytes;
-  if (line > 160 * 1024) throw GPUFFTError();
-  int lines = static_cast<int>(kLdsBudget / line);
+  auto magic = [](long long d) -> unsigned {
+    return d <= 1 ? 0u : static_cast<unsigned>(((1ull << 32) + d - 1) / d);
+  };
+  p.inplace = 1;
+  long long ns = 1;
+  for (int i = 0; i < p.np; ++i) {
+    p.radix[i] = r[i];
+    p.nsMagic[i] = magic(ns);
+    ns *= r[i];
+    if (!rt_codelet_radix(r[i])) p.inplace = 0;
+  }
+  p.nMagic = magic(n);
+  // the register staging of the in-place passes is sized for lines * n <= kRtElems
+  if (n > kRtElems) p.inplace = 0;
+  const std::size_t budget =
+      p.inplace ? static_cast<std::size_t>(kRtElems) * elemBytes : static_cast<std::size_t>(kLdsBudget);
+  // in-place plans keep one LDS region; ping-pong plans (a generic prime pass) two
+  const std::size_t regions = p.inplace ? 1 : 2;
+  if (regions * static_cast<std::size_t>(n + 1) * elemBytes > 160 * 1024) throw GPUFFTError();
+  // Lines: a power of two (line-fast engines split lane indices with shifts).
+  // Line stride: the passes run lines fastest, so consecutive lines start
+  // kMod / lines bank slots apart (an odd stride when lines >= kMod): a wave's
+  // accesses to one position of all lines hit distinct 16-B (fp64) / 8-B
+  // (fp32) slots of the 256-byte bank row.
+  const int kMod = static_cast<int>(256 / elemBytes);
+  int lines = static_cast<int>(budget / (regions * static_cast<std::size_t>(n + 1) * elemBytes));
   if (lines > kMaxThreads) lines = kMaxThreads;
-  // a power of two: line-fast engines split lane indices with shifts
+  if (lines < 1) lines = 1;
   p.linesLog2 = 0;
   while ((2 << p.linesLog2) <= lines) ++p.linesLog2;
-  p.lines = 1 << p.linesLog2;
+  for (;;) {
+    p.lines = 1 << p.linesLog2;
+    const int want = p.lines >= kMod ? 1 : kMod / p.lines;
+    p.ls = n;
+    while (p.ls % kMod != want % kMod) ++p.ls;
+    if (p.linesLog2 == 0 || regions * p.lines * static_cast<std::size_t>(p.ls) * elemBytes <= budget)
+      break;
+    --p.linesLog2;
+  }
   return p;
 }
 
