@@ -75,6 +75,11 @@ template <typename T>
 void TransformImpl<T>::forward(SpfftProcessingUnitType inputLocation, T* output,
                                SpfftScalingType scaling) {
   SPFFT_TIMED_SCOPE("forward");
+  if (scaling != SPFFT_NO_SCALING && scaling != SPFFT_FULL_SCALING) throw InvalidParameterError();
+  if (gpu_ && gpu_->forward_graph(inputLocation, output, scaling)) {
+    if (gpu_->synchronous()) gpu_->synchronize();
+    return;
+  }
   forward_xy(inputLocation);
   forward_exchange(false);
   forward_z(output, scaling);
@@ -84,6 +89,10 @@ void TransformImpl<T>::forward(SpfftProcessingUnitType inputLocation, T* output,
 template <typename T>
 void TransformImpl<T>::backward(const T* input, SpfftProcessingUnitType outputLocation) {
   SPFFT_TIMED_SCOPE("backward");
+  if (gpu_ && gpu_->backward_graph(input, outputLocation)) {
+    if (gpu_->synchronous()) gpu_->synchronize();
+    return;
+  }
   backward_z(input);
   backward_exchange(false);
   backward_xy(outputLocation);

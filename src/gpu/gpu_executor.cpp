@@ -46,8 +46,10 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
   chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
   interRing_ = chunkPlanes_ > 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
-  interRing_ = chunkPlanes_ > 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
+  // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
+  // launches in stream-ordered use (profiles/README.md, session 6)
+  graphsEnabled_ = env_int("SPFFT_GRAPH", 0, 0, 1) != 0;
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
@@ -285,6 +287,7 @@ GpuExecutor<T>::~GpuExecutor() {
   try {
     DeviceGuard guard(deviceId_);
     if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& g : graphs_) (void)hipGraphExecDestroy(g.exec);
     if (fusedFailHost_) (void)hipHostFree(fusedFailHost_);
   } catch (...) {
   }
@@ -401,8 +404,99 @@ void GpuExecutor<T>::wait_stream() {
   gpu_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
+// ------------------------------------------------------------- graph replay
+template <typename T>
+bool GpuExecutor<T>::graph_eligible() const {
+  // single rank only: exchanges (RCCL, peer barriers) stay outside graphs; the
+  // legacy default stream cannot be captured
+  return graphsEnabled_ && plan_->size == 1 && !fused_ && !poison_ && !gpu_sync_debug() &&
+         stream_ != nullptr;
+}
+
+template <typename T>
+template <class Enqueue>
+bool GpuExecutor<T>::replay(const GraphEntry& key, Enqueue enqueue) {
+  DeviceGuard guard(deviceId_);
+  GraphEntry* hit = nullptr;
+  for (auto& g : graphs_)
+    if (g.dir == key.dir && g.in == key.in && g.out == key.out && g.scaling == key.scaling &&
+        g.stream == key.stream)
+      hit = &g;
+  if (!hit) {
+    if (!warm_[key.dir]) {
+      // the first call of a direction runs eagerly (kernel attributes, lazy
+      // module loading happen outside any capture)
+      warm_[key.dir] = true;
+      return false;
+    }
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) {
+      capturing_ = true;
+      try {
+        enqueue();
+      } catch (...) {
+        ok = false;
+      }
+      capturing_ = false;
+      ok = hipStreamEndCapture(stream_, &graph) == hipSuccess && ok && graph;
+      if (ok) ok = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+      if (graph) (void)hipGraphDestroy(graph);
+    }
+    if (!ok) {
+      // capture unsupported here: run step-wise from now on
+      (void)hipGetLastError();
+      graphsEnabled_ = false;
+      if (exec) (void)hipGraphExecDestroy(exec);
+      return false;
+    }
+    if (graphs_.size() >= 8) {
+      (void)hipGraphExecDestroy(graphs_.front().exec);
+      graphs_.erase(graphs_.begin());
+    }
+    GraphEntry e = key;
+    e.exec = exec;
+    graphs_.push_back(e);
+    hit = &graphs_.back();
+  }
+  order_after_default_stream();
+  gpu_check(hipGraphLaunch(hit->exec, stream_), "hipGraphLaunch");
+  return true;
+}
+
+template <typename T>
+bool GpuExecutor<T>::backward_graph(const T* input, SpfftProcessingUnitType outputLocation) {
+  if (!graph_eligible() || outputLocation != SPFFT_PU_GPU) return false;
+  const bool any = plan_->numLocalElements > 0;
+  if (any && (!input || !is_device_pointer(input))) return false;
+  if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
+  SPFFT_TIMED_SCOPE("gpu_backward_graph");
+  const GraphEntry key{0, any ? input : nullptr, nullptr, 0, stream_, nullptr};
+  return replay(key, [&] {
+    backward_z(input);
+    backward_xy(SPFFT_PU_GPU);
+  });
+}
+
+template <typename T>
+bool GpuExecutor<T>::forward_graph(SpfftProcessingUnitType inputLocation, T* output,
+                                   SpfftScalingType scaling) {
+  if (!graph_eligible() || inputLocation != SPFFT_PU_GPU) return false;
+  const bool any = plan_->numLocalElements > 0;
+  if (any && (!output || !is_device_pointer(output))) return false;
+  if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
+  SPFFT_TIMED_SCOPE("gpu_forward_graph");
+  const GraphEntry key{1, nullptr, any ? output : nullptr, static_cast<int>(scaling), stream_, nullptr};
+  return replay(key, [&] {
+    forward_xy(SPFFT_PU_GPU);
+    forward_z(output, scaling);
+  });
+}
+
 template <typename T>
 void GpuExecutor<T>::order_after_default_stream() {
+  if (capturing_) return;
   // errors left behind by earlier (user) GPU work (reference: execution_gpu.cpp:251-253)
   if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
   if (ownStreamActive_) {
@@ -491,7 +585,7 @@ dev::XArgs GpuExecutor<T>::xargs() const {
 // first, so a kernel that reads an element nobody wrote shows up as NaN output.
 template <typename T>
 void GpuExecutor<T>::poison(bool backward) {
-  if (!poison_) return;
+  if (!poison_ || capturing_) return;
   auto fill = [&](typename GridImpl<T>::Slot slot) {
     gpu_check(hipMemsetAsync(grid_->device_slot(slot), 0xFF,
                              static_cast<std::size_t>(grid_->slot_elements(slot)) * sizeof(cx<T>),
@@ -520,7 +614,8 @@ void GpuExecutor<T>::backward_z(const T* input) {
   const cx<T>* values = reinterpret_cast<const cx<T>*>(input);
   if (p.numLocalElements > 0) {
     if (!input) throw InvalidParameterError();
-    if (!is_device_pointer(input)) {
+    // (a capture only runs for device-resident input: backward_graph)
+    if (!capturing_ && !is_device_pointer(input)) {
       cx<T>* st = staging(p.numLocalElements);
       gpu_check(hipMemcpyAsync(st, input, sizeof(cx<T>) * p.numLocalElements,
                                hipMemcpyHostToDevice, stream_),
@@ -726,7 +821,7 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
           ? static_cast<T>(1.0 / (static_cast<double>(p.dimX) * p.dimY * p.dimZ))
           : T(1);
   cx<T>* values = reinterpret_cast<cx<T>*>(output);
-  const bool hostOut = p.numLocalElements > 0 && !is_device_pointer(output);
+  const bool hostOut = p.numLocalElements > 0 && !capturing_ && !is_device_pointer(output);
   if (p.numLocalElements > 0 && !output) throw InvalidParameterError();
   if (hostOut) values = staging(p.numLocalElements);
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);

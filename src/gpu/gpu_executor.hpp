@@ -30,6 +30,14 @@ public:
   void forward_exchange(bool nonBlocking);
   void forward_z(T* output, SpfftScalingType scaling);
 
+  // Whole-direction hipGraph replay (single-rank transforms with device-resident
+  // input and output): the direction's launches are captured once per
+  // (pointers, scaling, stream) and replayed with one hipGraphLaunch. Returns
+  // false (nothing enqueued) when the call is not eligible; the caller then runs
+  // the step-wise path. Opt-in with SPFFT_GRAPH=1.
+  bool backward_graph(const T* input, SpfftProcessingUnitType outputLocation);
+  bool forward_graph(SpfftProcessingUnitType inputLocation, T* output, SpfftScalingType scaling);
+
   void synchronize();
   bool synchronous() const { return synchronous_; }
   // Execute on `stream` (nullptr = the legacy default stream); work is then
@@ -55,6 +63,17 @@ private:
   dev::YArgs yargs() const;
   dev::XArgs xargs() const;
   cx<T>* staging(std::size_t elems);
+  struct GraphEntry {
+    int dir;  // 0 backward, 1 forward
+    const void* in;
+    const void* out;
+    int scaling;
+    hipStream_t stream;
+    hipGraphExec_t exec;
+  };
+  bool graph_eligible() const;
+  template <class Enqueue>
+  bool replay(const GraphEntry& key, Enqueue enqueue);
   std::size_t space_bytes() const;
 
   std::shared_ptr<GridImpl<T>> grid_;
@@ -72,6 +91,10 @@ private:
   bool ownStreamActive_ = true;
   bool synchronous_ = true;
   std::unique_ptr<GpuEvent> event_;
+  bool capturing_ = false;      // order/poison steps are skipped inside a capture
+  bool graphsEnabled_ = false;  // SPFFT_GRAPH=1; off again after a failed capture
+  bool warm_[2] = {false, false};  // first call of a direction runs eagerly
+  std::vector<GraphEntry> graphs_;
 
   // device tables
   std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_, zRank_, segDispl_, segStride_, segZOff_;
