@@ -43,6 +43,11 @@ constexpr int kLdsBudget = SPFFT_LDS_BUDGET;
 #define SPFFT_RT_ELEMS 4096
 #endif
 constexpr int kRtElems = SPFFT_RT_ELEMS;
+// Workgroup size of the run-time engine kernels (tuning knob).
+#ifndef SPFFT_RT_THREADS
+#define SPFFT_RT_THREADS 256
+#endif
+constexpr int kRtThreads = SPFFT_RT_THREADS;
 
 template <typename T>
 struct LdsGeom;
@@ -335,7 +340,7 @@ struct FftRT {
   __device__ static int in_at(const RtPlan& p, int b, int pos) { return b * p.ls + pos; }
 
   // In-place Stockham pass of radix R over all lines of the block (blockDim.x ==
-  // kMaxThreads). Work item idx -> (line b = idx mod lines, butterfly j = idx /
+  // kRtThreads). Work item idx -> (line b = idx mod lines, butterfly j = idx /
   // lines): lines fastest, so a wave's LDS accesses spread over the lines' bank
   // offsets (plan stride, make_rt_plan). Every lane loads all its butterflies
   // into registers before the barrier and stores after it.
@@ -343,7 +348,7 @@ struct FftRT {
   __device__ static void pass_inplace(const RtPlan& p, cx<T>* buf, int ns, unsigned nsMagic,
                                       const cx<T>* __restrict__ tw) {
     constexpr int kElems = kRtElems;
-    constexpr int kIt = (kElems + R * kMaxThreads - 1) / (R * kMaxThreads);
+    constexpr int kIt = (kElems + R * kRtThreads - 1) / (R * kRtThreads);
     const int nb = p.n / R;
     const int total = nb << p.linesLog2;
     const int twStride = p.n / (ns * R);
@@ -351,7 +356,7 @@ struct FftRT {
     int dst[kIt];
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
-      const int idx = threadIdx.x + it * kMaxThreads;
+      const int idx = threadIdx.x + it * kRtThreads;
       if (idx < total) {
         const int b = idx & (p.lines - 1);
         const int j = idx >> p.linesLog2;
@@ -371,7 +376,7 @@ struct FftRT {
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
-      const int idx = threadIdx.x + it * kMaxThreads;
+      const int idx = threadIdx.x + it * kRtThreads;
       if (idx < total) {
 #pragma unroll
         for (int r = 0; r < R; ++r) buf[dst[it] + r * ns] = v[it][r];

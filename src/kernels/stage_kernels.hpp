@@ -106,10 +106,70 @@ __device__ __forceinline__ void st_stream_real(T* p, T v) {
 #endif
 }
 
+// Loads issued per lane before the first dependent LDS store: keeps U global
+// loads in flight per lane (memory-level parallelism for the gathers).
+constexpr int kGatherUnroll = 16;
+
+// for idx in [0, total): lds[dst(idx)] = load(idx) (dst < 0: skip), U loads in flight.
+template <typename T, class Load, class Dst>
+__device__ __forceinline__ void gather_to_lds(cx<T>* lds, int total, Load load, Dst dst) {
+  for (int base = threadIdx.x; base < total; base += blockDim.x * kGatherUnroll) {
+    cx<T> v[kGatherUnroll];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) v[u] = load(idx);
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) {
+        const int d = dst(idx);
+        if (d >= 0) lds[d] = v[u];
+      }
+    }
+  }
+}
+
+// for idx in [0, total): st(idx, lds[src(idx)]), U LDS reads in flight per lane
+// before the dependent global stores (a plain loop waits out the LDS latency of
+// every element).
+template <typename T, class Src, class St>
+__device__ __forceinline__ void scatter_from_lds(const cx<T>* lds, int total, Src src, St st) {
+  for (int base = threadIdx.x; base < total; base += blockDim.x * kGatherUnroll) {
+    cx<T> v[kGatherUnroll];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) v[u] = lds[src(idx)];
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int idx = base + u * static_cast<int>(blockDim.x);
+      if (idx < total) st(idx, v[u]);
+    }
+  }
+}
+
+
+// LDS -> global copy-out of a stage kernel: the run-time engines batch their LDS
+// reads (scatter_from_lds, measured +5-7% at 100^3-240^3); the compile-time
+// engines keep the plain loop (batching measured 1-2% slower at 128^3-256^3).
+template <class Eng, typename T, class Src, class St>
+__device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, St st) {
+  if constexpr (Eng::kBatchedCopy) {
+    scatter_from_lds(lds, total, src, st);
+  } else {
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) st(idx, lds[src(idx)]);
+  }
+}
+
 // ------------------------------------------------------------ engine adapters
 template <typename T, int N, int S, bool LF = false>
 struct CtEng {
   using F = FftCT<T, N, S, LF>;
+  static constexpr bool kBatchedCopy = false;
+  static constexpr int kBlock = kMaxThreads;
   __device__ int lines() const { return F::B; }
   __device__ int n() const { return N; }
   __device__ int in_at(int b, int pos) const { return F::in_at(b, pos); }
@@ -143,6 +203,8 @@ struct CtEng {
 // compile-time line-fast mapping; row engines walk positions fastest.
 template <typename T, int S, bool LF = false>
 struct RtEng {
+  static constexpr bool kBatchedCopy = true;
+  static constexpr int kBlock = kRtThreads;
   RtPlan p;
   __device__ int lines() const { return p.lines; }
   __device__ int n() const { return p.n; }
@@ -169,21 +231,19 @@ struct RtEng {
   template <class St>
   __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     const cx<T>* res = FftRT<T, S>::run_in_lds(p, lds, tw);
-    const int total = p.lines * p.n;
-    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-      int b, pos;
-      split(idx, b, pos);
-      st(b, pos, res[b * p.ls + pos]);
-    }
+    store_from(res, st);
   }
   template <class Ld>
   __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
-    const int total = p.lines * p.n;
-    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    gather_to_lds(lds, p.lines * p.n, [&](int idx) {
       int b, pos;
       split(idx, b, pos);
-      lds[b * p.ls + pos] = ld(b, pos);
-    }
+      return ld(b, pos);
+    }, [&](int idx) {
+      int b, pos;
+      split(idx, b, pos);
+      return b * p.ls + pos;
+    });
     __syncthreads();
     FftRT<T, S>::run_in_lds(p, lds, tw);
   }
@@ -193,12 +253,20 @@ struct RtEng {
   template <class Ld, class St>
   __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
     global_to_lds(lds, tw, ld);
-    const int total = p.lines * p.n;
-    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    store_from(lds + out_at(0, 0), st);
+  }
+  // result region res (index b * ls + pos) -> st(b, pos, v)
+  template <class St>
+  __device__ void store_from(const cx<T>* res, St st) const {
+    scatter_from_lds(res, p.lines * p.n, [&](int idx) {
       int b, pos;
       split(idx, b, pos);
-      st(b, pos, lds[out_at(b, pos)]);
-    }
+      return b * p.ls + pos;
+    }, [&](int idx, cx<T> v) {
+      int b, pos;
+      split(idx, b, pos);
+      st(b, pos, v);
+    });
   }
 };
 
@@ -209,6 +277,8 @@ struct RtEng {
 // filter for S = -1 and S = +1 [2m], twiddles of length m [m].
 template <typename T, int S>
 struct BlueEng {
+  static constexpr bool kBatchedCopy = true;
+  static constexpr int kBlock = kMaxThreads;
   RtPlan pm;  // length m, ls = m
   int nn;
   const cx<T>* chirp;
@@ -249,17 +319,17 @@ struct BlueEng {
   template <class St>
   __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__, St st) const {
     run(lds);
-    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
-      const int b = idx / nn, k = idx - b * nn;
-      st(b, k, lds[out_at(b, k)]);
-    }
+    store_from(lds, st);
   }
   template <class Ld>
   __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
-    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
-      const int b = idx / nn, k = idx - b * nn;
-      lds[in_at(b, k)] = ld(b, k);
-    }
+    gather_to_lds(lds, pm.lines * nn, [&](int idx) {
+      const int b = idx / nn;
+      return ld(b, idx - b * nn);
+    }, [&](int idx) {
+      const int b = idx / nn;
+      return in_at(b, idx - b * nn);
+    });
     __syncthreads();
     run(lds);
   }
@@ -267,10 +337,17 @@ struct BlueEng {
   template <class Ld, class St>
   __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
     global_to_lds(lds, tw, ld);
-    for (int idx = threadIdx.x; idx < pm.lines * nn; idx += blockDim.x) {
-      const int b = idx / nn, k = idx - b * nn;
-      st(b, k, lds[out_at(b, k)]);
-    }
+    store_from(lds, st);
+  }
+  template <class St>
+  __device__ void store_from(const cx<T>* lds, St st) const {
+    scatter_from_lds(lds, pm.lines * nn, [&](int idx) {
+      const int b = idx / nn;
+      return out_at(b, idx - b * nn);
+    }, [&](int idx, cx<T> v) {
+      const int b = idx / nn;
+      st(b, idx - b * nn, v);
+    });
   }
 };
 
@@ -330,31 +407,6 @@ __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
 #define SPFFT_LDS_DECL(T)                                         \
   extern __shared__ __attribute__((aligned(16))) char spfftSmem[]; \
   cx<T>* lds = reinterpret_cast<cx<T>*>(spfftSmem)
-
-// Loads issued per lane before the first dependent LDS store: keeps U global
-// loads in flight per lane (memory-level parallelism for the gathers).
-constexpr int kGatherUnroll = 16;
-
-// for idx in [0, total): lds[dst(idx)] = load(idx) (dst < 0: skip), U loads in flight.
-template <typename T, class Load, class Dst>
-__device__ __forceinline__ void gather_to_lds(cx<T>* lds, int total, Load load, Dst dst) {
-  for (int base = threadIdx.x; base < total; base += blockDim.x * kGatherUnroll) {
-    cx<T> v[kGatherUnroll];
-#pragma unroll
-    for (int u = 0; u < kGatherUnroll; ++u) {
-      const int idx = base + u * static_cast<int>(blockDim.x);
-      if (idx < total) v[u] = load(idx);
-    }
-#pragma unroll
-    for (int u = 0; u < kGatherUnroll; ++u) {
-      const int idx = base + u * static_cast<int>(blockDim.x);
-      if (idx < total) {
-        const int d = dst(idx);
-        if (d >= 0) lds[d] = v[u];
-      }
-    }
-  }
-}
 
 // Row side of a line-fast kernel: lanes walk along rows (row-contiguous global
 // loads) into the FFT lines in LDS; line-fast lanes would touch B rows with
@@ -475,7 +527,7 @@ __device__ __forceinline__ int find_run(const RunTable& t, int idx) {
 
 // ---------------------------------------------------------------- z stage
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     z_backward_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values, BT* __restrict__ out,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -526,7 +578,7 @@ __global__ void __launch_bounds__(kMaxThreads)
 }
 
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     z_forward_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                      T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -575,7 +627,7 @@ __device__ __forceinline__ int desc_offset(const StickDesc& q, int z) {
 }
 
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -611,7 +663,7 @@ __global__ void __launch_bounds__(kMaxThreads)
 }
 
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                           T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -638,7 +690,7 @@ __global__ void __launch_bounds__(kMaxThreads)
 // of one stick (coalesced) — with no LDS staging of the input. The x = 0
 // column of an R2C transform is gathered into LDS for the hermitian fill.
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -682,17 +734,20 @@ __global__ void __launch_bounds__(kMaxThreads)
     eng.lds_to_lds(lds, tw);
   }
   // rows of [z][column][y] are contiguous: coalesced copy-out
-  for (int idx = threadIdx.x; idx < zl * n; idx += blockDim.x) {
-    const int b = idx / n, pos = idx - b * n;
-    st_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos], lds[eng.out_at(b, pos)]);
-  }
+  copy_out<Eng>(lds, zl * n, [&](int idx) {
+    const int b = idx / n;
+    return eng.out_at(b, idx - b * n);
+  }, [&](int idx, cx<T> v) {
+    const int b = idx / n;
+    st_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + idx - b * n], v);
+  });
 }
 
 // Forward y stage, line-fast engine: lanes read rows of the intermediate and
 // write each stick's z-run of this plane block directly (consecutive lanes ->
 // consecutive z of one stick); no LDS staging on either side.
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     y_forward_kernel(Eng eng, YArgs a, const cx<T>* __restrict__ inter, BT* __restrict__ out,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -735,7 +790,7 @@ __global__ void __launch_bounds__(kMaxThreads)
 // zero for x without sticks; C2R completes the row by hermitian symmetry on
 // the fly. The result is written row-contiguous from LDS.
 template <class Eng, typename T, bool R2C>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     x_backward_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, void* __restrict__ space,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -761,20 +816,22 @@ __global__ void __launch_bounds__(kMaxThreads)
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
-  for (int idx = threadIdx.x; idx < yl * n; idx += blockDim.x) {
-    const int b = idx / n, pos = idx - b * n;
+  copy_out<Eng>(lds, yl * n, [&](int idx) {
+    const int b = idx / n;
+    return eng.out_at(b, idx - b * n);
+  }, [&](int idx, cx<T> v) {
     if (R2C)
-      st_stream_real(&static_cast<T*>(space)[row0 + idx], lds[eng.out_at(b, pos)].x);
+      st_stream_real(&static_cast<T*>(space)[row0 + idx], v.x);
     else
-      st_stream(&static_cast<cx<T>*>(space)[row0 + idx], lds[eng.out_at(b, pos)]);
-  }
+      st_stream(&static_cast<cx<T>*>(space)[row0 + idx], v);
+  });
 }
 
 // Forward x stage, line-fast engine: lanes read row segments of the space
 // domain and write the columns that hold sticks straight into [z][column][y]
 // (consecutive lanes -> consecutive y); R2C reads real rows.
 template <class Eng, typename T, bool R2C>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     x_forward_kernel(Eng eng, XArgs a, const void* __restrict__ space, cx<T>* __restrict__ inter,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
@@ -817,7 +874,7 @@ __global__ void __launch_bounds__(kMaxThreads)
 // with w = exp(S 2 pi i / n); the imaginary parts of X[0] and X[h] are ignored
 // (they cannot contribute to a real signal), as in the complex C2R path.
 template <class Eng, typename T>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     x_backward_c2r_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, T* __restrict__ space,
                           const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
   SPFFT_LDS_DECL(T);
@@ -868,14 +925,14 @@ __global__ void __launch_bounds__(kMaxThreads)
   eng.lds_to_lds(lds, twh);
   // the yl rows are contiguous in the space domain: one coalesced copy-out
   cx<T>* out = reinterpret_cast<cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
-  for (int idx = threadIdx.x; idx < yl * h; idx += blockDim.x) {
-    const int b = idx / h, m = idx - b * h;
-    st_stream(&out[idx], lds[eng.out_at(b, m)]);
-  }
+  copy_out<Eng>(lds, yl * h, [&](int idx) {
+    const int b = idx / h;
+    return eng.out_at(b, idx - b * h);
+  }, [&](int idx, cx<T> v) { st_stream(&out[idx], v); });
 }
 
 template <class Eng, typename T>
-__global__ void __launch_bounds__(kMaxThreads)
+__global__ void __launch_bounds__(Eng::kBlock)
     x_forward_r2c_kernel(Eng eng, XArgs a, const T* __restrict__ space, cx<T>* __restrict__ inter,
                          const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
   SPFFT_LDS_DECL(T);
@@ -959,7 +1016,7 @@ inline void with_engine(int n, F&& f) {
         return;
       }
       RtEng<T, S, LF> e{make_rt_plan(n, sizeof(cx<T>))};
-      f(e, kMaxThreads, e.p.lines,
+      f(e, kRtThreads, e.p.lines,
         std::size_t(e.p.inplace ? 1 : 2) * e.p.lines * e.p.ls * sizeof(cx<T>));
       return;
     }
