@@ -206,6 +206,49 @@ struct Dft<11, S, T> : DftOdd<11, S, T, fftc::C11, fftc::S11> {};
 template <int S, typename T>
 struct Dft<13, S, T> : DftOdd<13, S, T, fftc::C13, fftc::S13> {};
 
+// Coprime composites N = N1 N2 by the prime-factor (Good-Thomas) algorithm:
+// input n = (N2 n1 + N1 n2) mod N, output k with k = k1 (mod N1), k = k2 (mod N2).
+// No twiddles; after unrolling both index maps are register permutations.
+SPFFT_HD constexpr int pfa_inverse(int a, int m) {
+  int r = 1;
+  while ((a * r) % m != 1) ++r;
+  return r;
+}
+template <int N1, int N2, int S, typename T>
+struct DftPfa {
+  static SPFFT_HD void run(cx<T>* v) {
+    constexpr int N = N1 * N2;
+    constexpr int E1 = N2 * pfa_inverse(N2 % N1, N1);  // = 1 (mod N1), 0 (mod N2)
+    constexpr int E2 = N1 * pfa_inverse(N1 % N2, N2);  // = 0 (mod N1), 1 (mod N2)
+    cx<T> a[N2][N1];
+#pragma unroll
+    for (int n2 = 0; n2 < N2; ++n2) {
+#pragma unroll
+      for (int n1 = 0; n1 < N1; ++n1) a[n2][n1] = v[(N2 * n1 + N1 * n2) % N];
+      Dft<N1, S, T>::run(a[n2]);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < N1; ++k1) {
+      cx<T> b[N2];
+#pragma unroll
+      for (int n2 = 0; n2 < N2; ++n2) b[n2] = a[n2][k1];
+      Dft<N2, S, T>::run(b);
+#pragma unroll
+      for (int k2 = 0; k2 < N2; ++k2) v[(k1 * E1 + k2 * E2) % N] = b[k2];
+    }
+  }
+};
+template <int S, typename T>
+struct Dft<6, S, T> : DftPfa<2, 3, S, T> {};
+template <int S, typename T>
+struct Dft<10, S, T> : DftPfa<2, 5, S, T> {};
+template <int S, typename T>
+struct Dft<12, S, T> : DftPfa<4, 3, S, T> {};
+template <int S, typename T>
+struct Dft<15, S, T> : DftPfa<3, 5, S, T> {};
+template <int S, typename T>
+struct Dft<20, S, T> : DftPfa<4, 5, S, T> {};
+
 // Radices with a dedicated codelet; anything else runs through the generic
 // O(R) per-output path (any prime).
 SPFFT_HD constexpr bool has_codelet(int r) {

@@ -1,8 +1,11 @@
 // Radix factorisation and twiddle tables shared by host and GPU engines.
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <functional>
+#include <map>
 #include <vector>
 
 #include "fft/codelets.hpp"
@@ -39,6 +42,67 @@ inline std::vector<int> factorize_radices(int n) {
   }
   if (n > 1) r.push_back(n);
   return r;
+}
+
+// Radix plan of the host Stockham engine (and of the GPU run-time engine's fp64
+// in-place plans, see rt_pfa): the fewest passes over the codelets (incl. the
+// prime-factor composites 6, 10, 12, 15, 20), then the
+// fewest non-power-of-two passes, then larger radices first; power-of-two
+// radices lead. Factors without a codelet (primes > 13) keep their own passes.
+// Example: 240 = 16 * 15 (2 passes) instead of 16 * 3 * 5.
+inline std::vector<int> stockham_radices(int n) {
+  static const int kCand[] = {20, 16, 15, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2};
+  auto codelet = [&](int r) {
+    for (int c : kCand)
+      if (c == r) return true;
+    return false;
+  };
+  std::vector<int> rest;
+  long long m = 1;
+  for (int r : factorize_radices(n)) {
+    if (codelet(r))
+      m *= r;
+    else
+      rest.push_back(r);
+  }
+  struct Best {
+    int passes = 1 << 20, odd = 1 << 20;
+    std::vector<int> seq;  // descending
+  };
+  std::map<long long, Best> memo;
+  std::function<Best(long long)> solve = [&](long long v) -> Best {
+    Best best;
+    if (v == 1) {
+      best.passes = best.odd = 0;
+      return best;
+    }
+    auto it = memo.find(v);
+    if (it != memo.end()) return it->second;
+    for (int c : kCand) {
+      if (v % c) continue;
+      const Best sub = solve(v / c);
+      const int passes = sub.passes + 1, odd = sub.odd + ((c & (c - 1)) ? 1 : 0);
+      std::vector<int> seq = sub.seq;
+      seq.push_back(c);
+      std::sort(seq.begin(), seq.end(), [](int a, int b) { return a > b; });
+      if (passes < best.passes || (passes == best.passes && odd < best.odd) ||
+          (passes == best.passes && odd == best.odd && seq > best.seq)) {
+        best.passes = passes;
+        best.odd = odd;
+        best.seq = seq;
+      }
+    }
+    memo[v] = best;
+    return best;
+  };
+  const std::vector<int> seq = solve(m).seq;
+  std::vector<int> out;
+  for (int r : seq)
+    if (!(r & (r - 1))) out.push_back(r);
+  for (int r : seq)
+    if (r & (r - 1)) out.push_back(r);
+  out.insert(out.end(), rest.begin(), rest.end());
+  return out;
 }
 
 // tw[m] = exp(-2 pi i m / n), m in [0, n), rounded from long double.

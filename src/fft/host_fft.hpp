@@ -23,7 +23,7 @@ template <typename T>
 class HostFft {
 public:
   HostFft() = default;
-  explicit HostFft(int n) : n_(n), radices_(factorize_radices(n)), tw_(make_twiddles<T>(n)) {
+  explicit HostFft(int n) : n_(n), radices_(stockham_radices(n)), tw_(make_twiddles<T>(n)) {
     if (!radices_.empty() && radices_.back() > kBluesteinPrime) init_bluestein();
   }
 
@@ -116,12 +116,17 @@ private:
         case 3: pass<3, S>(src, dst, ns); break;
         case 4: pass<4, S>(src, dst, ns); break;
         case 5: pass<5, S>(src, dst, ns); break;
+        case 6: pass<6, S>(src, dst, ns); break;
         case 7: pass<7, S>(src, dst, ns); break;
         case 8: pass<8, S>(src, dst, ns); break;
         case 9: pass<9, S>(src, dst, ns); break;
+        case 10: pass<10, S>(src, dst, ns); break;
         case 11: pass<11, S>(src, dst, ns); break;
+        case 12: pass<12, S>(src, dst, ns); break;
         case 13: pass<13, S>(src, dst, ns); break;
+        case 15: pass<15, S>(src, dst, ns); break;
         case 16: pass<16, S>(src, dst, ns); break;
+        case 20: pass<20, S>(src, dst, ns); break;
         default: pass_generic<S>(src, dst, ns, r); break;
       }
       ns *= r;

@@ -329,10 +329,43 @@ struct RtPlan {
   unsigned nsMagic[16];  // ceil(2^32 / ns) of each pass (ns = product of the earlier radices)
 };
 
+// Prime-factor composite radices (6, 10, 12, 15, 20) in the run-time engine:
+// fewer passes per transform (240 = 16 * 15 instead of 16 * 5 * 3). Measured on
+// MI355X (profiles/README.md, session 12): +10-13% for fp64 at 100^3-240^3, but
+// -7% for fp32 at 240^3, where the larger pass switch costs more than the saved
+// pass. SPFFT_RT_PFA: -1 = per precision (fp64 on, fp32 off), 0 = off, 1 = on.
+#ifndef SPFFT_RT_PFA
+#define SPFFT_RT_PFA -1
+#endif
+__host__ __device__ constexpr bool rt_pfa(bool dbl) {
+  return SPFFT_RT_PFA < 0 ? dbl : SPFFT_RT_PFA != 0;
+}
+__host__ __device__ constexpr bool rt_composite_radix(int r) {
+  return r == 6 || r == 10 || r == 12 || r == 15 || r == 20;
+}
+
+// Butterflies per lane in an in-place pass of radix R: at most kRtElems /
+// kRtThreads (16) elements per lane for every radix, so the register staging is
+// the same for all radices (make_rt_plan sizes the lines so that each pass
+// fits; a plan that cannot falls back to the ping-pong passes).
+__host__ __device__ constexpr int rt_iters(int r) {
+  return (kRtElems / kRtThreads) / r > 0 ? (kRtElems / kRtThreads) / r : 1;
+}
+
 // Radices with a codelet (the in-place run-time passes are instantiated for these).
-__host__ __device__ constexpr bool rt_codelet_radix(int r) {
+__host__ __device__ constexpr bool rt_codelet_radix(int r, bool pfa) {
   return r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8 || r == 9 || r == 11 ||
-         r == 13 || r == 16;
+         r == 13 || r == 16 || (pfa && rt_composite_radix(r));
+}
+
+// A kernel-uniform value the compiler must treat as produced here: without it,
+// the per-radix products of p.n (n / R, r * n / R for every radix of the pass
+// switches) are hoisted into the kernel prologue, where they exceed the SGPR
+// file and spill (measured: 276-596 spilled SGPRs per run-time kernel).
+__device__ __forceinline__ int opaque_uniform(int v) {
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
 }
 
 template <typename T, int S>
@@ -347,11 +380,11 @@ struct FftRT {
   template <int R>
   __device__ static void pass_inplace(const RtPlan& p, cx<T>* buf, int ns, unsigned nsMagic,
                                       const cx<T>* __restrict__ tw) {
-    constexpr int kElems = kRtElems;
-    constexpr int kIt = (kElems + R * kRtThreads - 1) / (R * kRtThreads);
-    const int nb = p.n / R;
+    constexpr int kIt = rt_iters(R);
+    const int n = opaque_uniform(p.n);
+    const int nb = n / R;
     const int total = nb << p.linesLog2;
-    const int twStride = p.n / (ns * R);
+    const int twStride = n / (ns * R);
     cx<T> v[kIt][R];
     int dst[kIt];
 #pragma unroll
@@ -389,17 +422,30 @@ struct FftRT {
     int ns = 1;
     for (int i = 0; i < p.np; ++i) {
       const unsigned m = p.nsMagic[i];
-      switch (p.radix[i]) {
-        case 2: pass_inplace<2>(p, buf, ns, m, tw); break;
-        case 3: pass_inplace<3>(p, buf, ns, m, tw); break;
-        case 4: pass_inplace<4>(p, buf, ns, m, tw); break;
-        case 5: pass_inplace<5>(p, buf, ns, m, tw); break;
-        case 7: pass_inplace<7>(p, buf, ns, m, tw); break;
-        case 8: pass_inplace<8>(p, buf, ns, m, tw); break;
-        case 9: pass_inplace<9>(p, buf, ns, m, tw); break;
-        case 11: pass_inplace<11>(p, buf, ns, m, tw); break;
-        case 13: pass_inplace<13>(p, buf, ns, m, tw); break;
-        default: pass_inplace<16>(p, buf, ns, m, tw); break;
+      const int r = p.radix[i];
+      if (rt_pfa(sizeof(T) == 8) && rt_composite_radix(r)) {
+        if constexpr (rt_pfa(sizeof(T) == 8)) {
+          switch (r) {
+            case 6: pass_inplace<6>(p, buf, ns, m, tw); break;
+            case 10: pass_inplace<10>(p, buf, ns, m, tw); break;
+            case 12: pass_inplace<12>(p, buf, ns, m, tw); break;
+            case 15: pass_inplace<15>(p, buf, ns, m, tw); break;
+            default: pass_inplace<20>(p, buf, ns, m, tw); break;
+          }
+        }
+      } else {
+        switch (r) {
+          case 2: pass_inplace<2>(p, buf, ns, m, tw); break;
+          case 3: pass_inplace<3>(p, buf, ns, m, tw); break;
+          case 4: pass_inplace<4>(p, buf, ns, m, tw); break;
+          case 5: pass_inplace<5>(p, buf, ns, m, tw); break;
+          case 7: pass_inplace<7>(p, buf, ns, m, tw); break;
+          case 8: pass_inplace<8>(p, buf, ns, m, tw); break;
+          case 9: pass_inplace<9>(p, buf, ns, m, tw); break;
+          case 11: pass_inplace<11>(p, buf, ns, m, tw); break;
+          case 13: pass_inplace<13>(p, buf, ns, m, tw); break;
+          default: pass_inplace<16>(p, buf, ns, m, tw); break;
+        }
       }
       ns *= p.radix[i];
     }
@@ -408,8 +454,9 @@ struct FftRT {
   template <int R>
   __device__ static void pass(const RtPlan& p, const cx<T>* src, cx<T>* dst, int ns,
                               const cx<T>* __restrict__ tw) {
-    const int nb = p.n / R;
-    const int twStride = p.n / (ns * R);
+    const int n = opaque_uniform(p.n);
+    const int nb = n / R;
+    const int twStride = n / (ns * R);
     const int total = p.lines * nb;
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
       const int b = idx / nb, j = idx - b * nb;

@@ -233,8 +233,10 @@ struct RtEng {
     const cx<T>* res = FftRT<T, S>::run_in_lds(p, lds, tw);
     store_from(res, st);
   }
+  // input -> LDS at in_at(b, pos), no barrier (kernels with several input
+  // paths stage each and then run the FFT once: one inlined copy of the passes)
   template <class Ld>
-  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
+  __device__ void stage(cx<T>* lds, Ld ld) const {
     gather_to_lds(lds, p.lines * p.n, [&](int idx) {
       int b, pos;
       split(idx, b, pos);
@@ -244,6 +246,10 @@ struct RtEng {
       split(idx, b, pos);
       return b * p.ls + pos;
     });
+  }
+  template <class Ld>
+  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
+    stage(lds, ld);
     __syncthreads();
     FftRT<T, S>::run_in_lds(p, lds, tw);
   }
@@ -322,7 +328,7 @@ struct BlueEng {
     store_from(lds, st);
   }
   template <class Ld>
-  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
+  __device__ void stage(cx<T>* lds, Ld ld) const {
     gather_to_lds(lds, pm.lines * nn, [&](int idx) {
       const int b = idx / nn;
       return ld(b, idx - b * nn);
@@ -330,6 +336,10 @@ struct BlueEng {
       const int b = idx / nn;
       return in_at(b, idx - b * nn);
     });
+  }
+  template <class Ld>
+  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
+    stage(lds, ld);
     __syncthreads();
     run(lds);
   }
@@ -647,7 +657,14 @@ __global__ void __launch_bounds__(Eng::kBlock)
   auto store = [&](int b, int pos, cx<T> v) {
     if (b < nl) st_stream(&out[seg_index(a, s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
-  if (a.zeroStick >= s0 && a.zeroStick < s0 + nl) {
+  if constexpr (Eng::kBatchedCopy) {
+    // run-time engines: one staged path for every block (a single inlined copy
+    // of the pass switch keeps the kernel's register demand down)
+    eng.stage(lds, load);
+    __syncthreads();
+    if (a.zeroStick >= s0 && a.zeroStick < s0 + nl) hermitian_lines(eng, lds, a.zeroStick - s0, 1, n);
+    eng.lds_to_global(lds, tw, store);
+  } else if (a.zeroStick >= s0 && a.zeroStick < s0 + nl) {
     // block holding the (0,0) stick of an R2C transform: stage for the hermitian fill
     for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
       const int b = idx / n, z = idx - b * n;
@@ -713,12 +730,33 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
   __syncthreads();
   const int zl = min(B, a.L - z0);
-  if (c != a.colOfX0) {
-    eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
-      const int e = yEnt[pos];
-      if (e < 0 || b >= zl) return czero<T>();
-      return cvt<T>(ld_stream(&in[cBase[e] + b]));
-    });
+  auto load = [&](int b, int pos) -> cx<T> {
+    const int e = yEnt[pos];
+    if (e < 0 || b >= zl) return czero<T>();
+    return cvt<T>(ld_stream(&in[cBase[e] + b]));
+  };
+  if constexpr (Eng::kBatchedCopy) {
+    // run-time engines: stage either input path, then one FFT (a single inlined
+    // copy of the pass switch keeps the kernel's register demand down)
+    if (c != a.colOfX0) {
+      eng.stage(lds, load);
+      __syncthreads();
+    } else {
+      zero_lds(lds, eng.input_elems());
+      __syncthreads();
+      gather_to_lds(lds, ne * zl, [&](int idx) {
+        const int e = idx / zl, zz = idx - e * zl;
+        return cvt<T>(ld_stream(&in[cBase[e] + zz]));
+      }, [&](int idx) {
+        const int e = idx / zl, zz = idx - e * zl;
+        return eng.in_at(zz, cY[e]);
+      });
+      __syncthreads();
+      hermitian_lines(eng, lds, 0, B, n);
+    }
+    eng.lds_to_lds(lds, tw);
+  } else if (c != a.colOfX0) {
+    eng.global_to_lds(lds, tw, load);
   } else {
     zero_lds(lds, eng.input_elems());
     __syncthreads();

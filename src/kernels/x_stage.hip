@@ -9,6 +9,7 @@
 // after the HIP headers (codelets use __forceinline__ under hipcc)
 #include "fft/host_fft.hpp"
 
+
 namespace spfft {
 namespace dev {
 
@@ -73,10 +74,10 @@ template void launch_x_forward<float>(const XArgs&, bool, const void*, cx<float>
                                       const cx<float>*, const cx<float>*, hipStream_t);
 
 // ------------------------------------------------------------------ helpers
-RtPlan make_rt_plan(int n, std::size_t elemBytes) {
+namespace {
+RtPlan make_rt_plan_from(int n, std::size_t elemBytes, const std::vector<int>& r, bool pfa) {
   RtPlan p{};
   p.n = n;
-  const std::vector<int> r = factorize_radices(n);
   if (r.size() > 16) throw GPUFFTError();
   p.np = static_cast<int>(r.size());
   auto magic = [](long long d) -> unsigned {
@@ -88,11 +89,20 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
     p.radix[i] = r[i];
     p.nsMagic[i] = magic(ns);
     ns *= r[i];
-    if (!rt_codelet_radix(r[i])) p.inplace = 0;
+    if (!rt_codelet_radix(r[i], pfa)) p.inplace = 0;
   }
   p.nMagic = magic(n);
   // the register staging of the in-place passes is sized for lines * n <= kRtElems
+  // and rt_iters(R) butterflies per lane in a pass of radix R
   if (n > kRtElems) p.inplace = 0;
+  auto fits = [&](int log2) {
+    for (int i = 0; i < p.np; ++i)
+      if ((static_cast<long long>(n / p.radix[i]) << log2) >
+          static_cast<long long>(rt_iters(p.radix[i])) * kRtThreads)
+        return false;
+    return true;
+  };
+  if (!fits(0)) p.inplace = 0;  // a pass too long for one workgroup: ping-pong passes
   const std::size_t budget =
       p.inplace ? static_cast<std::size_t>(kRtElems) * elemBytes : static_cast<std::size_t>(kLdsBudget);
   // in-place plans keep one LDS region; ping-pong plans (a generic prime pass) two
@@ -109,6 +119,8 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
   if (lines < 1) lines = 1;
   p.linesLog2 = 0;
   while ((2 << p.linesLog2) <= lines) ++p.linesLog2;
+  if (p.inplace)
+    while (p.linesLog2 > 0 && !fits(p.linesLog2)) --p.linesLog2;
   for (;;) {
     p.lines = 1 << p.linesLog2;
     const int want = p.lines >= kMod ? 1 : kMod / p.lines;
@@ -119,6 +131,18 @@ RtPlan make_rt_plan(int n, std::size_t elemBytes) {
     --p.linesLog2;
   }
   return p;
+}
+}  // namespace
+
+RtPlan make_rt_plan(int n, std::size_t elemBytes) {
+  // fewest-pass plans over the composite codelets (6, 10, 12, 15, 20) where the
+  // kernels instantiate them; ping-pong plans (a generic prime pass, or lines too
+  // long for the in-place staging) keep the prime radices
+  if (rt_pfa(elemBytes == sizeof(cx<double>))) {
+    const RtPlan p = make_rt_plan_from(n, elemBytes, stockham_radices(n), true);
+    if (p.inplace) return p;
+  }
+  return make_rt_plan_from(n, elemBytes, factorize_radices(n), false);
 }
 
 std::string describe_engine(int n, bool dbl, bool lineFast) {

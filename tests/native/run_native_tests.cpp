@@ -49,6 +49,14 @@ SPFFT_TEST(host_c2c_sweep) {
         }
 }
 
+// lengths whose plans use the prime-factor composite codelets 6, 10, 12, 15, 20
+SPFFT_TEST(host_composite_lengths) {
+  const int dims[][3] = {{6, 10, 15}, {20, 30, 12}, {45, 60, 2}, {90, 4, 120}, {240, 3, 5},
+                         {180, 7, 36}, {360, 2, 1}};
+  unsigned seed = 100;
+  for (const auto& d : dims) check_c2c(SPFFT_PU_HOST, d[0], d[1], d[2], (seed & 1) != 0, seed++);
+}
+
 SPFFT_TEST(gpu_c2c_sweep) {
   if (!have_gpu()) return;
   const int sizes[] = {1, 2, 11, 16, 32, 100};

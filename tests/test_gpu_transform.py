@@ -160,6 +160,40 @@ def test_single_precision(gpu, dims):
     assert max_rel_error(out.cpu().numpy(), ref) < 2e-5
 
 
+@pytest.mark.parametrize("dims", [(240, 6, 10), (15, 20, 30), (60, 90, 12), (120, 45, 7),
+                                  (180, 36, 20), (100, 30, 16)])
+@pytest.mark.parametrize("ttype", ["c2c", "r2c"])
+@pytest.mark.parametrize("single", [False, True])
+def test_composite_radices(gpu, dims, ttype, single):
+    """Mixed-radix lengths in every stage (z row engine, y/x line-fast engines,
+    packed-real x); the fp64 plans use the prime-factor codelets 6, 10, 12, 15,
+    20 (rt_pfa), the fp32 plans the prime radices."""
+    import torch
+    rng = np.random.default_rng(17)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.8, 0.8, nx, ny, nz, r2c)[0]
+    if r2c:
+        vals = dense_forward(rng.standard_normal((nz, ny, nx)), idx, dims)
+    else:
+        vals = _rand_vals(rng, len(idx))
+    vals = vals.astype(np.complex64 if single else np.complex128)
+    grid = (sp.GridFloat if single else sp.Grid)(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    ref = dense_backward(idx, vals.astype(np.complex128), dims, r2c=r2c)
+    tol = 2e-5 if single else 1e-12
+    assert max_rel_error(out.cpu().numpy(), ref) < tol
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    space = space.astype((np.float32 if r2c else np.complex64) if single else
+                         (np.float64 if r2c else np.complex128))
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space.astype(np.complex128), idx, dims)) < tol
+
+
 def test_host_pointers_on_gpu_transform(gpu):
     """GPU transform with host input/output and host space domain (staging paths)."""
     rng = np.random.default_rng(4)
