@@ -59,3 +59,28 @@ def test_torch_dist_ipc_3ranks_repeated(gpu):
     # many back-to-back transforms with fresh data: a stale read of an earlier
     # exchange (missing barrier / visibility) shows as a mismatch
     _launch(3, "UNBUFFERED", "--iters=12", "--dims=64,60,48", expect="ipc")
+
+
+def _bench_json(out):
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(lines) == 1, out[-4000:]  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_driver_launch_2ranks(gpu):
+    # the round driver's multi-GPU launch line, rehearsed with 2 ranks on one
+    # device: JSON contract fields and a checked round trip on every rank
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--size", "96", "--check"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    rec = _bench_json(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["higher_is_better"] is True
+    assert rec["config"]["check_error"]["roundtrip"] < 1e-12
