@@ -165,6 +165,15 @@ def main():
     check = None
     if a.check:
         check = _check(a, sp, t, values, gidx, dims, ttype, world)
+        if dist is not None:
+            # every rank's round trip counts: rank 0 reports the worst one
+            e = torch.tensor([check["roundtrip"]], dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            check["roundtrip"] = float(e.item())
+            check["ranks_checked"] = world
+    # ranks that share a device (rehearsal on a small box) are not a multi-GPU
+    # measurement: record how many distinct devices the job really used
+    n_devices = min(world, ndev)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * a.steps / elapsed
     if rank == 0:
@@ -191,6 +200,8 @@ def main():
                 "num_frequency_values": int(len(gidx)),
                 "exchange": a.exchange,
                 "data_plane": plane,
+                "distinct_devices": n_devices,
+                "shared_device": n_devices < world,
                 "sync": a.sync,
                 "check_error": check,
                 "step": "1 backward + 1 forward transform",

@@ -282,6 +282,9 @@ struct FftCT {
 
   // Result delivered to store(b, pos, value); stores of a lane are at
   // pos = t + k*TP + r*N/RL (consecutive lanes -> consecutive positions).
+  // Contract: run() stores only the lane's own line (b == lane_line()); the z
+  // forward kernel keeps that line's stick descriptor in registers and relies
+  // on it (asserted there in debug builds).
   __device__ static int lane_line() { return LF ? threadIdx.x % B : threadIdx.x / TP; }
   __device__ static int lane_pos() { return LF ? threadIdx.x / B : threadIdx.x % TP; }
 

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cassert>
 #include <type_traits>
 
 #include "gpu/gpu_runtime.hpp"
@@ -689,8 +690,11 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int nl = min(B, a.numSticks - s0);
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
-    // LDS round trip (65.1 vs 67.4 us at 256^3; the same change in the backward
-    // kernel, whose value loads are on the critical path, measured 81 -> 104 us)
+    // LDS round trip (69.6 -> 65.0 us at 256^3, profiles/r1_s14/zdesc_ab/
+    // summary.txt; the same change in the backward kernel, whose value loads
+    // are on the critical path, measured 81 -> 104 us). This relies on the
+    // compile-time engines' run() storing only the lane's own line
+    // (b == lane_line()); the assert guards that contract in debug builds.
     const int lb = Eng::F::lane_line();
     StickDesc q{};
     if (lb < nl) q = a.desc[s0 + lb];
@@ -698,24 +702,25 @@ __global__ void __launch_bounds__(Eng::kBlock)
       if (b >= nl) return czero<T>();
       return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
     }, [&](int b, int pos, cx<T> v) {
+      assert(b == lb);
       if (b >= nl) return;
       const int j = desc_offset(q, pos);
       if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
     });
-    return;
+  } else {
+    StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
+    for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
+    __syncthreads();
+    eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
+      if (b >= nl) return czero<T>();
+      return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
+    }, [&](int b, int pos, cx<T> v) {
+      if (b >= nl) return;
+      const StickDesc& q = d[b];
+      const int j = desc_offset(q, pos);
+      if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
+    });
   }
-  StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
-  __syncthreads();
-  eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
-    if (b >= nl) return czero<T>();
-    return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
-  }, [&](int b, int pos, cx<T> v) {
-    if (b >= nl) return;
-    const StickDesc& q = d[b];
-    const int j = desc_offset(q, pos);
-    if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
-  });
 }
 
 // ---------------------------------------------------------------- y stage

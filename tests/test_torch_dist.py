@@ -83,4 +83,11 @@ def test_bench_driver_launch_2ranks(gpu):
     rec = _bench_json(r.stdout)
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
     assert rec["value"] > 0 and rec["higher_is_better"] is True
+    # the reported round-trip error is the MAX over both ranks
+    assert rec["config"]["check_error"]["ranks_checked"] == 2
     assert rec["config"]["check_error"]["roundtrip"] < 1e-12
+    # both ranks ran on the one card of the test box: flagged as a rehearsal
+    import torch
+    ndev = torch.cuda.device_count()
+    assert rec["config"]["distinct_devices"] == min(2, ndev)
+    assert rec["config"]["shared_device"] is (ndev < 2)
