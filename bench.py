@@ -24,6 +24,10 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# transforms/s of the reference's vendor-FFT calls alone on one MI355X, 256^3
+# C2C fp64 r = N/2 (tools/ref_pipeline_bench.py)
+REF_FFT_ONLY_256 = 2210.2
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -176,6 +180,11 @@ def main():
     n_devices = min(world, ndev)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * a.steps / elapsed
+    # the reference's FFT calls alone (rocFFT via torch.fft)
+    # on one MI355X, an upper bound on its throughput for the headline config;
+    # no measured reference exists for other configs or for N > 1 GPUs
+    headline = (n == 256 and a.cutoff == 0.5 and a.type == "c2c" and not single)
+    vs_baseline = rate / REF_FFT_ONLY_256 if (headline and world == 1) else None
     if rank == 0:
         if a.timing:
             print(sp.timing_report(), file=sys.stderr)
@@ -189,7 +198,7 @@ def main():
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            "vs_baseline": vs_baseline,
             "dtype": "fp32" if single else "fp64",
             "data": "synthetic (random complex values on the spherical-cutoff index set)",
             "config": {

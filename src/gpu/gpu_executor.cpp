@@ -102,11 +102,11 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     // collective data-plane setup happens at plan time
     peerWrites_ = grid_->device_comm().peer_writes();
     if (peerWrites_) build_peer_tables();
-    // exchange pipelining. Automatic choice: chunks only while the average
-    // per-peer message of a chunk stays >= 4 MB (smaller RCCL messages lose
-    // more link efficiency than the overlap gains), at most 4; computed from
-    // global quantities so every rank agrees. SPFFT_EXCH_CHUNKS forces a count
-    // (rank 0's value is used everywhere).
+    // exchange pipelining over plane chunks (build_chunk_plan). Automatic
+    // choice: chunks only while the average per-peer message of a chunk stays
+    // >= 4 MB (smaller RCCL messages lose link efficiency), at most 4; computed
+    // from global quantities so every rank agrees. SPFFT_EXCH_CHUNKS forces a
+    // count (rank 0's value is used everywhere).
     const double perPeer = static_cast<double>(p.totalSticks) * p.dimZ * eb /
                            (static_cast<double>(p.size) * p.size);
     int chunks = static_cast<int>(std::min(4.0, std::max(1.0, std::floor(perPeer / (4 << 20)))));
@@ -147,79 +147,72 @@ template <typename T>
 void GpuExecutor<T>::build_chunk_plan(int K) {
   const IndexPlan& p = *plan_;
   const int P = p.size, me = p.rank;
-  const std::int64_t eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   // K depends on global quantities only: every rank issues the same number of
-  // all-to-all rounds (ranks with few sticks get empty chunks)
-  const int ncols = p.num_columns();
-  if (ncols < 1) return;
-  K = std::max(1, std::min(K, ncols));
-  // backward: chunk k = sticks [S_q k / K, S_q (k+1) / K) of every rank q
-  auto sb = [&](int q, int k) { return static_cast<std::int64_t>(p.sticksPerRank[q]) * k / K; };
-  bwdStickBounds_.resize(K + 1);
-  for (int k = 0; k <= K; ++k) bwdStickBounds_[k] = static_cast<int>(sb(me, k));
-  bwdChunks_.assign(K, ChunkXfer{});
+  // all-to-all rounds (a rank with fewer planes than K gets empty chunks)
+  if (layout_.buffered || K < 2) return;
+  const i64 eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+  auto pb = [&](int r, int k) -> i64 { return static_cast<i64>(p.planesPerRank[r]) * k / K; };
+  const i64 S = p.local_sticks();
+  // stick side: segment v = k*P + r holds (local sticks) x (chunk k of rank r's
+  // planes); the z stage finds a plane's segment through the zRank table
+  const int NV = K * P;
+  std::vector<long long> segDispl(NV), segStride(NV);
+  std::vector<int> segZOff(NV), zSeg(p.dimZ, 0);
+  i64 off = 0;
   for (int k = 0; k < K; ++k) {
-    ChunkXfer& c = bwdChunks_[k];
     for (int r = 0; r < P; ++r) {
-      const std::int64_t s0 = sb(me, k), s1 = sb(me, k + 1);
-      c.sd.push_back((layout_.stickDispl[r] + s0 * layout_.stickStride[r]) * eb);
-      c.sc.push_back((s1 - s0) * layout_.stickStride[r] * eb);
-      const std::int64_t q0 = sb(r, k), q1 = sb(r, k + 1);
-      c.rd.push_back((layout_.slabDispl[r] + q0 * layout_.slabStride) * eb);
-      c.rc.push_back((q1 - q0) * layout_.slabStride * eb);
+      const int v = k * P + r;
+      const i64 n = pb(r, k + 1) - pb(r, k);
+      segDispl[v] = off;
+      segStride[v] = n;
+      segZOff[v] = p.planeOffsets[r] + static_cast<int>(pb(r, k));
+      for (i64 z = 0; z < n; ++z) zSeg[segZOff[v] + z] = v;
+      off += S * n;
     }
   }
-  // forward: chunk k = columns [cb_k, cb_{k+1}) balanced by stick entries; every
-  // rank's sticks inside a column range are a contiguous run of its local sticks
-  // (columns ascend in x, local sticks ascend in x*dimY+y)
-  fwdColBounds_.assign(K + 1, ncols);
-  fwdColBounds_[0] = 0;
-  const std::int64_t total = p.colOffsets[ncols];
-  for (int k = 1; k < K; ++k) {
-    int c = fwdColBounds_[k - 1];
-    while (c < ncols && static_cast<std::int64_t>(p.colOffsets[c]) * K < total * k) ++c;
-    fwdColBounds_[k] = c;
-  }
-  std::vector<std::vector<std::int64_t>> rowB(K, std::vector<std::int64_t>(P, 0)),
-      rowE(K, std::vector<std::int64_t>(P, 0));
+  if (off != layout_.stickTotal) throw InternalError();
+  // slab side: block (k, q) holds (sticks of rank q) x (chunk k of my planes)
+  std::vector<i64> slabDispl(NV);
+  off = 0;
   for (int k = 0; k < K; ++k) {
-    std::vector<std::int64_t> lo(P, std::numeric_limits<std::int64_t>::max()), hi(P, -1), cnt(P, 0);
-    for (int e = p.colOffsets[fwdColBounds_[k]]; e < p.colOffsets[fwdColBounds_[k + 1]]; ++e) {
-      const int r = p.colRank[e];
-      lo[r] = std::min<std::int64_t>(lo[r], p.colLocal[e]);
-      hi[r] = std::max<std::int64_t>(hi[r], p.colLocal[e]);
-      ++cnt[r];
+    const i64 lk = pb(me, k + 1) - pb(me, k);
+    for (int q = 0; q < P; ++q) {
+      slabDispl[k * P + q] = off;
+      off += static_cast<i64>(p.sticksPerRank[q]) * lk;
     }
+  }
+  if (off != layout_.slabTotal) throw InternalError();
+  planeBounds_.resize(K + 1);
+  for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
+  colBaseChunk_.clear();
+  chunks_.assign(K, ChunkXfer{});
+  for (int k = 0; k < K; ++k) {
+    const i64 lk = pb(me, k + 1) - pb(me, k);
+    // entry e at local plane z of chunk k: base + z (z in [pb_k, pb_k+1))
+    std::vector<long long> cb(p.colY.size());
+    for (std::size_t e = 0; e < p.colY.size(); ++e)
+      cb[e] = slabDispl[k * P + p.colRank[e]] + static_cast<i64>(p.colLocal[e]) * lk - pb(me, k);
+    colBaseChunk_.emplace_back();
+    upload(colBaseChunk_.back(), cb);
+    ChunkXfer& c = chunks_[k];
     for (int r = 0; r < P; ++r) {
-      if (cnt[r] == 0) continue;
-      if (hi[r] - lo[r] + 1 != cnt[r]) {  // not contiguous: no forward pipelining
-        fwdColBounds_.clear();
-        break;
-      }
-      rowB[k][r] = lo[r];
-      rowE[k][r] = hi[r] + 1;
-    }
-    if (fwdColBounds_.empty()) break;
-  }
-  if (!fwdColBounds_.empty()) {
-    fwdChunks_.assign(K, ChunkXfer{});
-    for (int k = 0; k < K; ++k) {
-      ChunkXfer& c = fwdChunks_[k];
-      for (int r = 0; r < P; ++r) {
-        // send: my slab-side rows of rank r's sticks in this column chunk
-        c.sd.push_back((layout_.slabDispl[r] + rowB[k][r] * layout_.slabStride) * eb);
-        c.sc.push_back((rowE[k][r] - rowB[k][r]) * layout_.slabStride * eb);
-        // receive: my sticks' rows of this chunk from every rank
-        c.rd.push_back((layout_.stickDispl[r] + rowB[k][me] * layout_.stickStride[r]) * eb);
-        c.rc.push_back((rowE[k][me] - rowB[k][me]) * layout_.stickStride[r] * eb);
-      }
+      const int v = k * P + r;
+      c.sd.push_back(segDispl[v] * eb);
+      c.sc.push_back(S * segStride[v] * eb);
+      c.rd.push_back(slabDispl[v] * eb);
+      c.rc.push_back(static_cast<i64>(p.sticksPerRank[r]) * lk * eb);
     }
   }
+  upload(zRank_, zSeg);
+  upload(segDispl_, segDispl);
+  upload(segStride_, segStride);
+  upload(segZOff_, segZOff);
   exchChunks_ = K;
-  commStream_.reset(new GpuStream());
+  commStream_.reset(new GpuStream(true));
   chunkEvents_.clear();
   for (int k = 0; k < K; ++k) chunkEvents_.emplace_back(new GpuEvent());
   commDone_.reset(new GpuEvent());
+  zDone_.reset(new GpuEvent());
 }
 
 template <typename T>
@@ -229,14 +222,23 @@ void GpuExecutor<T>::pipelined_exchange(bool backward) {
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   DeviceComm& dc = grid_->device_comm();
   hipStream_t cs = commStream_->get();
-  const auto& chunks = backward ? bwdChunks_ : fwdChunks_;
+  if (backward) {
+    // the whole z stage precedes every chunk; the y/x stages of chunk k wait on
+    // chunkEvents_[k] (backward_xy)
+    zDone_->record(stream_);
+    zDone_->wait_on(cs);
+    for (int k = 0; k < exchChunks_; ++k) {
+      const ChunkXfer& c = chunks_[k];
+      dc.alltoallv(stick, c.sc.data(), c.sd.data(), slab, c.rc.data(), c.rd.data(), cs);
+      chunkEvents_[k]->record(cs);
+    }
+    return;
+  }
+  // chunk k's y stage recorded chunkEvents_[k] (forward_xy)
   for (int k = 0; k < exchChunks_; ++k) {
     chunkEvents_[k]->wait_on(cs);
-    const ChunkXfer& c = chunks[k];
-    if (backward)
-      dc.alltoallv(stick, c.sc.data(), c.sd.data(), slab, c.rc.data(), c.rd.data(), cs);
-    else
-      dc.alltoallv(slab, c.sc.data(), c.sd.data(), stick, c.rc.data(), c.rd.data(), cs);
+    const ChunkXfer& c = chunks_[k];
+    dc.alltoallv(slab, c.rc.data(), c.rd.data(), stick, c.sc.data(), c.sd.data(), cs);
   }
   commDone_->record(cs);
   commDone_->wait_on(stream_);
@@ -636,20 +638,12 @@ void GpuExecutor<T>::backward_z(const T* input) {
     a.segDispl = segDisplRemote_->data<long long>();
     a.remote = 1;
   }
-  const bool chunked = exchChunks_ > 1 && !bwdChunks_.empty();
-  for (int k = 0; k < (chunked ? exchChunks_ : 1); ++k) {
-    if (chunked) {
-      a.stickBegin = bwdStickBounds_[k];
-      a.numSticks = bwdStickBounds_[k + 1];
-    }
-    if (floatExchange_)
-      dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
-                                           twZ_->data<cx<T>>(), stream_);
-    else
-      dev::launch_z_backward<T, cx<T>>(a, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
-                                       stream_);
-    if (chunked) chunkEvents_[k]->record(stream_);
-  }
+  if (floatExchange_)
+    dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
+                                         twZ_->data<cx<T>>(), stream_);
+  else
+    dev::launch_z_backward<T, cx<T>>(a, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
+                                     stream_);
 }
 
 template <typename T>
@@ -675,7 +669,7 @@ void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
     grid_->device_comm().complete_writes(stream_);
     return;
   }
-  if (exchChunks_ > 1 && !bwdChunks_.empty()) {
+  if (exchChunks_ > 1) {
     pipelined_exchange(true);
     return;
   }
@@ -699,6 +693,33 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
                                static_cast<const cx<T>*>(grid_->device_slot(GridImpl<T>::kStickSide)),
                                static_cast<cx<T>*>(space), fscratch_->data<cx<T>>(),
                                twY_->data<cx<T>>(), twX_->data<cx<T>>(), stream_);
+    if (outputLocation == SPFFT_PU_HOST) {
+      gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
+                               hipMemcpyDeviceToHost, stream_),
+                "hipMemcpyAsync");
+    }
+    return;
+  }
+  if (exchChunks_ > 1) {
+    // pipelined exchange: the y/x stages of chunk k start when it has arrived
+    for (int k = 0; k < exchChunks_; ++k) {
+      chunkEvents_[k]->wait_on(stream_);
+      auto ya = yargs();
+      auto xa = xargs();
+      ya.zBegin = xa.zBegin = planeBounds_[k];
+      ya.L = xa.L = planeBounds_[k + 1];
+      if (ya.L <= ya.zBegin) continue;
+      ya.colBase = colBaseChunk_[k]->data<long long>();
+      if (floatExchange_)
+        dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
+                                             twY_->data<cx<T>>(), stream_);
+      else
+        dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), interBase,
+                                         twY_->data<cx<T>>(), stream_);
+      dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, interBase, space,
+                                twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
+                                stream_);
+    }
     if (outputLocation == SPFFT_PU_HOST) {
       gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
                                hipMemcpyDeviceToHost, stream_),
@@ -762,6 +783,29 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides
   if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
+  if (exchChunks_ > 1) {
+    // pipelined exchange: chunk k's all-to-all starts when its y stage is done
+    for (int k = 0; k < exchChunks_; ++k) {
+      auto ya = yargs();
+      auto xa = xargs();
+      ya.zBegin = xa.zBegin = planeBounds_[k];
+      ya.L = xa.L = planeBounds_[k + 1];
+      if (ya.L > ya.zBegin) {
+        ya.colBase = colBaseChunk_[k]->data<long long>();
+        dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
+                                 twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
+                                 stream_);
+        if (floatExchange_)
+          dev::launch_y_forward<T, cx<float>>(ya, interBase, static_cast<cx<float>*>(slab),
+                                              twY_->data<cx<T>>(), stream_);
+        else
+          dev::launch_y_forward<T, cx<T>>(ya, interBase, static_cast<cx<T>*>(slab),
+                                          twY_->data<cx<T>>(), stream_);
+      }
+      chunkEvents_[k]->record(stream_);
+    }
+    return;
+  }
   const int L = plan_->local_planes();
   const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
   for (int zb = 0; zb < L; zb += chunk) {
@@ -777,22 +821,12 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
-    // column chunks of the pipelined exchange (chunk k's all-to-all starts when
-    // its y stage is done)
-    const bool chunked = exchChunks_ > 1 && !fwdChunks_.empty();
-    for (int k = 0; k < (chunked ? exchChunks_ : 1); ++k) {
-      if (chunked) {
-        ya.colBegin = fwdColBounds_[k];
-        ya.colEnd = fwdColBounds_[k + 1];
-      }
-      if (floatExchange_)
-        dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
-                                            twY_->data<cx<T>>(), stream_);
-      else
-        dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab),
-                                        twY_->data<cx<T>>(), stream_);
-      if (chunked) chunkEvents_[k]->record(stream_);
-    }
+    if (floatExchange_)
+      dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+                                          twY_->data<cx<T>>(), stream_);
+    else
+      dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
+                                      stream_);
   }
 }
 
@@ -804,7 +838,7 @@ void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
     grid_->device_comm().complete_writes(stream_);
     return;
   }
-  if (exchChunks_ > 1 && !fwdChunks_.empty()) {
+  if (exchChunks_ > 1) {
     pipelined_exchange(false);
     return;
   }

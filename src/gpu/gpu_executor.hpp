@@ -115,18 +115,24 @@ private:
   void setup_fused();
   void check_fused();
 
-  // Pipelined exchange (RCCL / loopback data planes): the z stage (backward) and
-  // the y stage (forward) run in K chunks of sticks / columns; chunk k's
-  // all-to-all runs on commStream_ while chunk k+1 is computed.
+  // Pipelined exchange (RCCL / loopback data planes, compact layout): every
+  // rank's planes are split into K chunks and both exchange buffers are laid
+  // out chunk-major, so chunk k is one contiguous block per peer. Backward: the
+  // z stage runs whole, chunk k's all-to-all runs on commStream_ and the y/x
+  // stages of chunk k start as soon as it has arrived (while chunk k+1 is in
+  // flight). Forward: the x/y stages run per chunk and chunk k's all-to-all
+  // starts when its y stage is done. The exchange overlaps the y and x stages,
+  // two thirds of the compute, in both directions.
   struct ChunkXfer {
-    std::vector<std::int64_t> sc, sd, rc, rd;  // bytes per rank
+    std::vector<std::int64_t> sc, sd, rc, rd;  // bytes per rank (backward direction)
   };
   int exchChunks_ = 1;
-  std::vector<int> bwdStickBounds_, fwdColBounds_;
-  std::vector<ChunkXfer> bwdChunks_, fwdChunks_;
+  std::vector<int> planeBounds_;  // K+1 local plane bounds of the chunks
+  std::vector<ChunkXfer> chunks_;
+  std::vector<std::unique_ptr<DeviceBuffer>> colBaseChunk_;  // y-stage entry bases per chunk
   std::unique_ptr<GpuStream> commStream_;
   std::vector<std::unique_ptr<GpuEvent>> chunkEvents_;
-  std::unique_ptr<GpuEvent> commDone_;
+  std::unique_ptr<GpuEvent> commDone_, zDone_;
   std::unique_ptr<DeviceBuffer> twX_, twXh_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;
   std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;

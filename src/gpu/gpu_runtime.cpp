@@ -72,7 +72,15 @@ DeviceGuard::~DeviceGuard() {
   if (switched_) (void)hipSetDevice(previous_);
 }
 
-GpuStream::GpuStream() { gpu_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"); }
+GpuStream::GpuStream(bool highPriority) {
+  int lo = 0, hi = 0;
+  if (highPriority && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+    gpu_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreate");
+    return;
+  }
+  (void)hipGetLastError();
+  gpu_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+}
 GpuStream::~GpuStream() {
   if (stream_ && !process_exiting()) (void)hipStreamDestroy(stream_);
 }

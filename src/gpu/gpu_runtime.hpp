@@ -40,7 +40,10 @@ private:
 
 class GpuStream {
 public:
-  GpuStream();  // non-blocking stream on the current device
+  // non-blocking stream on the current device; highPriority: the device's
+  // greatest stream priority (communication streams, so their kernels are
+  // dispatched ahead of queued compute workgroups)
+  explicit GpuStream(bool highPriority = false);
   ~GpuStream();
   GpuStream(const GpuStream&) = delete;
   GpuStream& operator=(const GpuStream&) = delete;
