@@ -79,6 +79,10 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(colY_, p.colY);
   std::vector<long long> cb(layout_.colEntryBase.begin(), layout_.colEntryBase.end());
   upload(colBase_, cb);
+  // opt-in: measured slower for the backward y stage (97 -> 123 us at 256^3,
+  // profiles/r2_s1/col_table.txt), no change forward
+  colTables_ = env_int("SPFFT_COL_TABLE", 0, 0, 1) != 0;
+  upload_col_addr(colAddr_, cb);
   upload(colX_, p.colX);
   upload(twX_, make_twiddles<T>(p.dimX));
   // packed-real x stage for R2C with even dimX (SPFFT_R2C_PACKED=0 disables)
@@ -144,6 +148,24 @@ void GpuExecutor<T>::log_plan() const {
 }
 
 template <typename T>
+void GpuExecutor<T>::upload_col_addr(std::unique_ptr<DeviceBuffer>& buf,
+                                     const std::vector<long long>& colBase) {
+  const IndexPlan& p = *plan_;
+  const i64 elems = static_cast<i64>(p.num_columns()) * p.dimY;
+  // 8 bytes per (column, y): 512 KB at 256^3, 2 MB at 512^3; very large grids
+  // keep the LDS-staged entry lists
+  if (!colTables_ || elems < 1 || elems > (i64(1) << 23)) {
+    buf.reset();
+    return;
+  }
+  std::vector<long long> t(static_cast<std::size_t>(elems), dev::kNoColEntry);
+  for (int c = 0; c < p.num_columns(); ++c)
+    for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e)
+      t[static_cast<std::size_t>(c) * p.dimY + p.colY[e]] = colBase[e];
+  upload(buf, t);
+}
+
+template <typename T>
 void GpuExecutor<T>::build_chunk_plan(int K) {
   const IndexPlan& p = *plan_;
   const int P = p.size, me = p.rank;
@@ -185,6 +207,7 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
   planeBounds_.resize(K + 1);
   for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
   colBaseChunk_.clear();
+  colAddrChunk_.clear();
   chunks_.assign(K, ChunkXfer{});
   for (int k = 0; k < K; ++k) {
     const i64 lk = pb(me, k + 1) - pb(me, k);
@@ -194,6 +217,8 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
       cb[e] = slabDispl[k * P + p.colRank[e]] + static_cast<i64>(p.colLocal[e]) * lk - pb(me, k);
     colBaseChunk_.emplace_back();
     upload(colBaseChunk_.back(), cb);
+    colAddrChunk_.emplace_back();
+    upload_col_addr(colAddrChunk_.back(), cb);
     ChunkXfer& c = chunks_[k];
     for (int r = 0; r < P; ++r) {
       const int v = k * P + r;
@@ -281,6 +306,7 @@ void GpuExecutor<T>::build_peer_tables() {
   for (std::size_t k = 0; k < p.colY.size(); ++k)
     cb[k] = base[p.colRank[k]] + static_cast<i64>(p.colLocal[k]) * layout_.slabStride;
   upload(colBaseRemote_, cb);
+  upload_col_addr(colAddrRemote_, cb);
 }
 
 template <typename T>
@@ -564,6 +590,7 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
+  a.colAddr = colAddr_ ? colAddr_->data<long long>() : nullptr;
   return a;
 }
 
@@ -710,6 +737,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L <= ya.zBegin) continue;
       ya.colBase = colBaseChunk_[k]->data<long long>();
+      ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
       if (floatExchange_)
         dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
                                              twY_->data<cx<T>>(), stream_);
@@ -792,6 +820,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L > ya.zBegin) {
         ya.colBase = colBaseChunk_[k]->data<long long>();
+        ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
         dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
                                  twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
                                  stream_);
@@ -817,6 +846,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
         interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (peerWrites_) {
       ya.colBase = colBaseRemote_->data<long long>();
+      ya.colAddr = colAddrRemote_ ? colAddrRemote_->data<long long>() : nullptr;
       ya.remote = 1;
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,

@@ -110,6 +110,7 @@ struct CtShape<128> {
   static constexpr int E = 16, R0 = 16, R1 = 8, R2 = 1;
 };
 #ifndef SPFFT_CT256_E
+#define SPFFT_CT256_DEFAULT_SHAPE 1
 #define SPFFT_CT256_E 16
 #endif
 #if SPFFT_CT256_E == 8
@@ -157,6 +158,28 @@ struct CtShapeT<float, 1024> {
   static constexpr int E = 32, R0 = 16, R1 = 16, R2 = 4, kBudget = 80 * 1024;
 };
 
+// Shape per stage kind: S = +1 backward / -1 forward, LF = line-fast (y and x
+// stages) vs row-mapped (z stage). For complex<double> N = 256 the radix-8
+// shape (E = 8, 256 threads per 8 lines) doubles the waves per SIMD that the
+// LDS budget allows, which the memory-bound stages turn into bandwidth:
+// measured on MI355X at 256^3 (profiles/r2_s1/shape_ab.txt) x backward 97.6 ->
+// 93.1 us, z backward 79.2 -> 75.3 us, x/y forward -1 us; the forward z stage
+// is slower with it (65.7 -> 71.7 us) and keeps E = 16.
+struct CtShape256E8 {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4, kBudget = kLdsBudget;
+};
+template <typename T, int N, int S, bool LF>
+struct CtShapeSel : std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::type {};
+// (a build with an explicit -DSPFFT_CT256_E=... uses that one shape everywhere)
+#if defined(SPFFT_CT256_DEFAULT_SHAPE)
+template <>
+struct CtShapeSel<double, 256, 1, false> : CtShape256E8 {};
+template <>
+struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
+template <>
+struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
+#endif
+
 struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 
 // largest power of two <= b, at most 16 (line-fast lane mapping)
@@ -194,8 +217,9 @@ __host__ __device__ constexpr int lf_padded_stride(int n, int b) {
 template <typename T, int N, int S, bool LF = false>
 struct FftCT {
   // line-fast engines (column access) take the precision-specific shape; the
-  // row-mapped engine of the z stage keeps the default (fewer VGPRs per lane)
-  using Sh = typename std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::type;
+  // row-mapped engine of the z stage keeps the default (fewer VGPRs per lane);
+  // CtShapeSel overrides per stage kind where measured faster
+  using Sh = CtShapeSel<T, N, S, LF>;
   static constexpr int E = Sh::E;
   static constexpr int TP = N / E;  // lanes per line
   static constexpr int LS0 = padded_stride<T>(N);

@@ -38,6 +38,8 @@ struct ZArgs {
   int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
 };
 
+constexpr long long kNoColEntry = -(1LL << 62);
+
 struct YArgs {
   int ncols;     // columns of the [z][column][y] intermediate (its row count per plane)
   int colBegin;  // column range processed: [colBegin, colEnd) (exchange pipelining chunks)
@@ -50,6 +52,12 @@ struct YArgs {
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
+  // optional dense [ncols][n] table: colBase of the entry at (column, y),
+  // kNoColEntry where the column has no stick at y (bases of the peer-write
+  // tables are offsets to other GPUs' buffers and may be negative). Lets a workgroup address its sticks
+  // without staging the column's entry list in LDS (no prologue of dependent
+  // loads and barriers before the main loads).
+  const long long* colAddr;
   int remote;  // forward stores reach peers' memory: release system-wide at exit
 };
 

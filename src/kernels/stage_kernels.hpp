@@ -724,19 +724,14 @@ __global__ void __launch_bounds__(Eng::kBlock)
 }
 
 // ---------------------------------------------------------------- y stage
-// Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
-// loads straight from the stick side — consecutive lanes read consecutive z
-// of one stick (coalesced) — with no LDS staging of the input. The x = 0
-// column of an R2C transform is gathered into LDS for the hermitian fill.
+// y backward through the column's entry list staged in LDS (no dense table,
+// or the x = 0 column of an R2C transform, which needs the hermitian fill).
+// Ends with the FFT result in LDS.
 template <class Eng, typename T, typename BT>
-__global__ void __launch_bounds__(Eng::kBlock)
-    y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
-                      const cx<T>* __restrict__ tw) {
-  SPFFT_LDS_DECL(T);
+__device__ void y_backward_entries(const Eng& eng, const YArgs& a, const BT* __restrict__ in,
+                                   const cx<T>* __restrict__ tw, cx<T>* lds, int c, int z0, int zl) {
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = a.colBegin + blockIdx.x;
-  const int z0 = a.zBegin + blockIdx.y * B;
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
   long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
@@ -751,7 +746,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     cY[e] = y;
   }
   __syncthreads();
-  const int zl = min(B, a.L - z0);
   auto load = [&](int b, int pos) -> cx<T> {
     const int e = yEnt[pos];
     if (e < 0 || b >= zl) return czero<T>();
@@ -793,6 +787,41 @@ __global__ void __launch_bounds__(Eng::kBlock)
     hermitian_lines(eng, lds, 0, B, n);
     eng.lds_to_lds(lds, tw);
   }
+}
+
+
+// Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
+// loads straight from the stick side — consecutive lanes read consecutive z
+// of one stick (coalesced) — with no LDS staging of the input. The x = 0
+// column of an R2C transform is gathered into LDS for the hermitian fill.
+template <class Eng, typename T, typename BT>
+__global__ void __launch_bounds__(Eng::kBlock)
+    y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
+                      const cx<T>* __restrict__ tw) {
+  SPFFT_LDS_DECL(T);
+  const int B = eng.lines();
+  const int n = eng.n();
+  const int c = a.colBegin + blockIdx.x;
+  const int z0 = a.zBegin + blockIdx.y * B;
+  const int zl = min(B, a.L - z0);
+  if (a.colAddr && c != a.colOfX0) {
+    // dense entry table: the stick loads start right away
+    const long long* ca = a.colAddr + static_cast<long long>(c) * n;
+    auto load = [&](int b, int pos) -> cx<T> {
+      const long long base = ca[pos];
+      if (base == kNoColEntry || b >= zl) return czero<T>();
+      return cvt<T>(ld_stream(&in[base + z0 + b]));
+    };
+    if constexpr (Eng::kBatchedCopy) {
+      eng.stage(lds, load);
+      __syncthreads();
+      eng.lds_to_lds(lds, tw);
+    } else {
+      eng.global_to_lds(lds, tw, load);
+    }
+  } else {
+    y_backward_entries(eng, a, in, tw, lds, c, z0, zl);
+  }
   // rows of [z][column][y] are contiguous: coalesced copy-out
   copy_out<Eng>(lds, zl * n, [&](int idx) {
     const int b = idx / n;
@@ -815,6 +844,27 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   const int c = a.colBegin + blockIdx.x;
   const int z0 = a.zBegin + blockIdx.y * B;
+  const int zl = min(B, a.L - z0);
+  auto load = [&](int b, int pos) -> cx<T> {
+    if (b >= zl) return czero<T>();
+    return ld_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
+  };
+  if (a.colAddr) {
+    // dense entry table: no prologue in front of the row loads
+    const long long* ca = a.colAddr + static_cast<long long>(c) * n;
+    auto st = [&](int b, int pos, cx<T> v) {
+      const long long base = ca[pos];
+      if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+    };
+#if SPFFT_ROW_STAGE
+    stage_rows(eng, lds, zl, n, load);
+    eng.lds_to_global(lds, tw, st);
+#else
+    eng.global_to_global(lds, tw, load, st);
+#endif
+    release_remote(a.remote);
+    return;
+  }
   const int k0 = a.colOffsets[c];
   const int ne = a.colOffsets[c + 1] - k0;
   long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
@@ -826,11 +876,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     yEnt[a.colY[k0 + e]] = e;
   }
   __syncthreads();
-  const int zl = min(B, a.L - z0);
-  auto load = [&](int b, int pos) -> cx<T> {
-    if (b >= zl) return czero<T>();
-    return ld_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
-  };
   auto store = [&](int b, int pos, cx<T> v) {
     const int e = yEnt[pos];
     if (e >= 0 && b < zl) st_stream(&out[cBase[e] + b], cvt<typename BT::value_type>(v));
@@ -842,6 +887,23 @@ __global__ void __launch_bounds__(Eng::kBlock)
   eng.global_to_global(lds, tw, load, store);
 #endif
   release_remote(a.remote);
+}
+
+// x stage column lookup: every x of [0, nFreq) holds a column (e.g. a sphere
+// of radius N/2) -> colX is the identity and no table is built; otherwise the
+// workgroup stages the x -> column table in LDS. The table build is a
+// dependent global load plus two barriers in front of every workgroup's main
+// loads, so the dense case skips it.
+__device__ __forceinline__ bool x_dense(const XArgs& a) { return a.ncols == a.nFreq; }
+__device__ __forceinline__ void build_xcol(const XArgs& a, int* xCol, int count) {
+  if (x_dense(a)) return;
+  for (int x = threadIdx.x; x < count; x += blockDim.x) xCol[x] = -1;
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
+  __syncthreads();
+}
+__device__ __forceinline__ int xcol_of(const XArgs& a, const int* xCol, int x) {
+  return x_dense(a) ? (x < a.nFreq ? x : -1) : xCol[x];
 }
 
 // ---------------------------------------------------------------- x stage
@@ -859,19 +921,16 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
-  __syncthreads();
-  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
-  __syncthreads();
+  build_xcol(a, xCol, n);
   const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   const int yl = min(B, a.Y - y0);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
-      const int c = xCol[n - pos];
+      const int c = xcol_of(a, xCol, n - pos);
       return c < 0 ? czero<T>() : conj(ld_inter(&src[static_cast<long long>(c) * a.interStride + b]));
     }
-    const int c = xCol[pos];
+    const int c = xcol_of(a, xCol, pos);
     return c < 0 ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
@@ -900,10 +959,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  for (int x = threadIdx.x; x < n; x += blockDim.x) xCol[x] = -1;
-  __syncthreads();
-  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
-  __syncthreads();
+  build_xcol(a, xCol, n);
   const int yl = min(B, a.Y - y0);
   cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   auto load = [&](int b, int pos) -> cx<T> {
@@ -913,7 +969,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return ld_stream(&static_cast<const cx<T>*>(space)[row + pos]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
-    const int c = xCol[pos];
+    const int c = xcol_of(a, xCol, pos);
     if (c >= 0 && b < yl) st_inter(&dst[static_cast<long long>(c) * a.interStride + b], v);
   };
 #if SPFFT_ROW_STAGE
@@ -946,24 +1002,21 @@ __global__ void __launch_bounds__(Eng::kBlock)
   // LDS: FFT lines | X[h] (Nyquist) per line | xCol table
   cx<T>* nyq = reinterpret_cast<cx<T>*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   int* xCol = reinterpret_cast<int*>(nyq + B);
-  for (int x = threadIdx.x; x <= h; x += blockDim.x) xCol[x] = -1;
-  __syncthreads();
-  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
-  __syncthreads();
+  build_xcol(a, xCol, h + 1);
   const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
   const int yl = min(B, a.Y - y0);
   // columns X[0..h] of the block's rows, each element loaded once (lanes run
   // over rows: contiguous column segments)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
     const int k = idx / B, b = idx - k * B;
-    const int c = xCol[k];
+    const int c = xcol_of(a, xCol, k);
     return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   }, [&](int idx) {
     const int k = idx / B;
     return eng.in_at(idx - k * B, k);
   });
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const int c = xCol[h];
+    const int c = xcol_of(a, xCol, h);
     nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
   }
   __syncthreads();
@@ -1002,10 +1055,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int zl = a.zBegin + blockIdx.y;
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  for (int x = threadIdx.x; x <= h; x += blockDim.x) xCol[x] = -1;
-  __syncthreads();
-  for (int c = threadIdx.x; c < a.ncols; c += blockDim.x) xCol[a.colX[c]] = c;
-  __syncthreads();
+  build_xcol(a, xCol, h + 1);
   const int yl = min(B, a.Y - y0);
   const cx<T>* row0 = reinterpret_cast<const cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
   stage_rows(eng, lds, yl, h, [&](int b, int m) { return ld_stream(row0 + static_cast<long long>(b) * h + m); });
@@ -1014,7 +1064,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   // post pass: lanes run over rows first, so the column stores are contiguous
   for (int idx = threadIdx.x; idx < B * (h + 1); idx += blockDim.x) {
     const int b = idx % B, k = idx / B;
-    const int c = xCol[k];
+    const int c = xcol_of(a, xCol, k);
     if (c < 0 || b >= yl) continue;
     const cx<T> yk = lds[eng.out_at(b, k == h ? 0 : k)];
     const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
