@@ -723,6 +723,19 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
 }
 
+// y-stage tile order. SPFFT_Y_ZFAST=1: plane blocks fastest in the grid, so
+// the workgroups in flight cover a few whole columns: each stick is read (or
+// written) entirely while it is open in the DRAM row buffers, and the
+// [z][column][y] rows of a plane are written as one contiguous run.
+#ifndef SPFFT_Y_ZFAST
+#define SPFFT_Y_ZFAST 1
+#endif
+__device__ __forceinline__ int y_tile_col() { return SPFFT_Y_ZFAST ? blockIdx.y : blockIdx.x; }
+__device__ __forceinline__ int y_tile_zblock() { return SPFFT_Y_ZFAST ? blockIdx.x : blockIdx.y; }
+inline dim3 y_grid(int cols, int zblocks) {
+  return SPFFT_Y_ZFAST ? dim3(zblocks, cols) : dim3(cols, zblocks);
+}
+
 // ---------------------------------------------------------------- y stage
 // y backward through the column's entry list staged in LDS (no dense table,
 // or the x = 0 column of an R2C transform, which needs the hermitian fill).
@@ -801,8 +814,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = a.colBegin + blockIdx.x;
-  const int z0 = a.zBegin + blockIdx.y * B;
+  const int c = a.colBegin + y_tile_col();
+  const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   if (a.colAddr && c != a.colOfX0) {
     // dense entry table: the stick loads start right away
@@ -842,8 +855,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = a.colBegin + blockIdx.x;
-  const int z0 = a.zBegin + blockIdx.y * B;
+  const int c = a.colBegin + y_tile_col();
+  const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
