@@ -646,6 +646,9 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   const int s0 = a.stickBegin + blockIdx.x * B;
   const int nl = min(B, a.numSticks - s0);
+  auto store = [&](int b, int pos, cx<T> v) {
+    if (b < nl) st_stream(&out[seg_index(a, s0 + b, pos)], cvt<typename BT::value_type>(v));
+  };
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
   __syncthreads();
@@ -654,9 +657,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const StickDesc& q = d[b];
     const int j = desc_offset(q, z);
     return j < 0 ? czero<T>() : ld_values(&values[q.valueStart + j]);
-  };
-  auto store = [&](int b, int pos, cx<T> v) {
-    if (b < nl) st_stream(&out[seg_index(a, s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
   if constexpr (Eng::kBatchedCopy) {
     // run-time engines: one staged path for every block (a single inlined copy

@@ -54,7 +54,11 @@ SPFFT_TEST(host_composite_lengths) {
   const int dims[][3] = {{6, 10, 15}, {20, 30, 12}, {45, 60, 2}, {90, 4, 120}, {240, 3, 5},
                          {180, 7, 36}, {360, 2, 1}};
   unsigned seed = 100;
-  for (const auto& d : dims) check_c2c(SPFFT_PU_HOST, d[0], d[1], d[2], (seed & 1) != 0, seed++);
+  for (const auto& d : dims) {
+    const bool centred = (seed & 1) != 0;
+    check_c2c(SPFFT_PU_HOST, d[0], d[1], d[2], centred, seed);
+    ++seed;
+  }
 }
 
 SPFFT_TEST(gpu_c2c_sweep) {
