@@ -170,6 +170,23 @@ struct CtShape256E8 {
 };
 template <typename T, int N, int S, bool LF>
 struct CtShapeSel : std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::type {};
+// N = 128 likewise (radices 8, 8, 2; 16 lanes per line): 256^3 R2C 6467 ->
+// 6820 transforms/s (packed-real x stage on N/2 = 128), 128^3 C2C 23770 ->
+// 25550 (profiles/r2_s1/shape_ab.txt)
+#ifndef SPFFT_CT128_E8
+#define SPFFT_CT128_E8 1
+#endif
+#if SPFFT_CT128_E8
+struct CtShape128E8 {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 2, kBudget = kLdsBudget;
+};
+template <>
+struct CtShapeSel<double, 128, 1, false> : CtShape128E8 {};
+template <>
+struct CtShapeSel<double, 128, 1, true> : CtShape128E8 {};
+template <>
+struct CtShapeSel<double, 128, -1, true> : CtShape128E8 {};
+#endif
 // (a build with an explicit -DSPFFT_CT256_E=... uses that one shape everywhere)
 #if defined(SPFFT_CT256_DEFAULT_SHAPE)
 template <>
