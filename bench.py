@@ -4,9 +4,15 @@
 One step = one backward (frequency -> space) + one forward (space -> frequency)
 transform of the 256^3 grid with the spherical cutoff |k| <= N/2 (≈8.78 M
 frequency values, 51,431 z-sticks), fp64 complex, exactly like one repeat of
-the reference benchmark (reference: tests/programs/benchmark.cpp:85-88);
-transforms/sec = 2 * steps / elapsed. Data is synthetic (random values),
+the reference benchmark (reference: tests/programs/benchmark.cpp:85-88).
+Data is synthetic (random values),
 inputs and outputs live in GPU memory ("gpu-gpu" mode of the reference).
+
+A step runs 4 independent transforms of that problem (--transforms, the
+reference benchmark's -m, tests/programs/benchmark.cpp:142, 84-96): multi_transform_backward +
+multi_transform_forward, one HIP stream per transform, so one transform's
+all-to-all and kernel tails overlap the others' kernels. transforms/sec =
+2 * transforms * steps / elapsed. --transforms 1 times single calls.
 
 Multi-GPU: launched by torch.distributed.run, one rank per GPU; z-sticks and
 xy-planes are split evenly over ranks and the pencil <-> slab redistribution
@@ -40,6 +46,10 @@ def parse():
                     choices=["compact", "compactFloat", "buffered", "bufferedFloat", "unbuffered"])
     ap.add_argument("--precision", default="double", choices=["double", "single"])
     ap.add_argument("--type", default="c2c", choices=["c2c", "r2c"])
+    ap.add_argument("--transforms", type=int, default=4,
+                    help="independent transforms per step, run with multi_transform_backward/"
+                         "forward on one stream each (the reference benchmark's -m): one "
+                         "transform's all-to-all overlaps the others' FFT kernels")
     ap.add_argument("--timing", action="store_true", help="print the native timing tree")
     ap.add_argument("--check", action="store_true",
                     help="after timing: round-trip error on every rank and, on one rank, the "
@@ -118,30 +128,46 @@ def main():
     GridCls = sp.GridFloat if single else sp.Grid
     cdtype = torch.complex64 if single else torch.complex128
 
-    if world == 1:
-        local = gidx
-        zlen = n
-        grid = GridCls(n, n, n, n * n, sp.ProcessingUnit.GPU, 1)
-        t = grid.create_transform(sp.ProcessingUnit.GPU, ttype, n, n, n, n, local)
-    else:
+    def make_transform():
+        # every transform owns its grid (multi_transform rejects shared grids)
+        if world == 1:
+            g = GridCls(n, n, n, n * n, sp.ProcessingUnit.GPU, 1)
+            return g, g.create_transform(sp.ProcessingUnit.GPU, ttype, n, n, n, n, gidx), gidx
         from spfft_amd.parallel import TorchDistComm, make_distributed
-        comm = TorchDistComm()
-        setup = make_distributed(comm, dims, gidx, processing_unit=sp.ProcessingUnit.GPU,
+        setup = make_distributed(TorchDistComm(), dims, gidx, processing_unit=sp.ProcessingUnit.GPU,
                                  transform_type=ttype, exchange_type=exch, single=single)
-        grid, t, local, zlen = setup.grid, setup.transform, setup.indices, setup.z_length
+        return setup.grid, setup.transform, setup.indices
+
+    T = max(1, a.transforms)
+    made = [make_transform() for _ in range(T)]
+    grids = [m[0] for m in made]
+    ts = [m[1] for m in made]
+    local = made[0][2]
+    grid, t = grids[0], ts[0]
 
     plane = grid.data_plane if world > 1 else "none"
+    streams = []
     if a.sync == "stream":
-        t.set_stream(torch.cuda.current_stream(), synchronous=False)
+        if T == 1:
+            t.set_stream(torch.cuda.current_stream(), synchronous=False)
+        else:
+            streams = [torch.cuda.Stream() for _ in range(T)]
+            for tr, st in zip(ts, streams):
+                tr.set_stream(st, synchronous=False)
 
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
-    values = torch.randn(len(local), dtype=cdtype, device=dev, generator=gen)
-    out = torch.empty_like(values)
+    vals = [torch.randn(len(local), dtype=cdtype, device=dev, generator=gen) for _ in range(T)]
+    outs = [torch.empty_like(v) for v in vals]
+    values, out = vals[0], outs[0]
 
     def step():
-        t.backward(values)
-        t.forward(None, output=out)
+        if T == 1:
+            t.backward(values)
+            t.forward(None, output=out)
+        else:
+            sp.multi_transform_backward(ts, vals)
+            sp.multi_transform_forward(ts, outputs=outs)
 
     def barrier():
         torch.cuda.synchronize()
@@ -179,7 +205,7 @@ def main():
     # measurement: record how many distinct devices the job really used
     n_devices = min(world, ndev)
     ms_per_step = 1e3 * elapsed / a.steps
-    rate = 2.0 * a.steps / elapsed
+    rate = 2.0 * T * a.steps / elapsed
     # the reference's FFT calls alone (rocFFT via torch.fft)
     # on one MI355X, an upper bound on its throughput for the headline config;
     # no measured reference exists for other configs or for N > 1 GPUs
@@ -203,7 +229,8 @@ def main():
             "data": "synthetic (random complex values on the spherical-cutoff index set)",
             "config": {
                 "model": f"sparse 3D FFT {n}^3 {a.type.upper()} spherical cutoff r={a.cutoff}*N",
-                "global_batch": 2,
+                "global_batch": 2 * T,
+                "transforms_per_step": T,
                 "seq_len": n,
                 "parallelism": f"slab/pencil x{world} ({a.exchange} all-to-all)",
                 "num_frequency_values": int(len(gidx)),
@@ -213,7 +240,8 @@ def main():
                 "shared_device": n_devices < world,
                 "sync": a.sync,
                 "check_error": check,
-                "step": "1 backward + 1 forward transform",
+                "step": ("1 backward + 1 forward transform" if T == 1 else
+                         f"multi_transform backward + forward of {T} independent transforms"),
             },
         }
         print(json.dumps(rec), flush=True)
