@@ -45,7 +45,9 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
   chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
-  interRing_ = chunkPlanes_ > 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
+  // [z][column][y] (plane-major, default) or [column][z][y] intermediate
+  interColMajor_ = env_int("SPFFT_INTER_CMAJOR", 0, 0, 1) != 0;
+  interRing_ = chunkPlanes_ > 0 && !interColMajor_ && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
   // launches in stream-ordered use (profiles/README.md, session 6)
@@ -576,6 +578,18 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
 }
 
 template <typename T>
+void GpuExecutor<T>::inter_strides(long long& zStride, long long& cStride) const {
+  const IndexPlan& p = *plan_;
+  if (interColMajor_) {
+    zStride = interStride_;
+    cStride = static_cast<long long>(p.local_planes()) * interStride_;
+  } else {
+    zStride = static_cast<long long>(p.num_columns()) * interStride_;
+    cStride = interStride_;
+  }
+}
+
+template <typename T>
 dev::YArgs GpuExecutor<T>::yargs() const {
   const IndexPlan& p = *plan_;
   dev::YArgs a{};
@@ -587,6 +601,7 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.n = p.dimY;
   a.colOfX0 = p.type == SPFFT_TRANS_R2C ? p.colOfX0 : -1;
   a.interStride = interStride_;
+  inter_strides(a.interZStride, a.interCStride);
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
@@ -605,6 +620,7 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   a.nFreq = p.dimXFreq;
   a.ncols = p.num_columns();
   a.interStride = interStride_;
+  inter_strides(a.interZStride, a.interCStride);
   a.colX = colX_ ? colX_->data<int>() : nullptr;
   return a;
 }

@@ -49,6 +49,9 @@ struct YArgs {
   int n;  // dimY
   int colOfX0;  // column needing the x=0 plane hermitian fill, -1 for none
   long long interStride;  // row stride of the [z][column][y] intermediate (>= n)
+  // row (z, column c) of the intermediate starts at z * interZStride + c * interCStride
+  // (plane-major: ncols*interStride, interStride; column-major: interStride, L*interStride)
+  long long interZStride, interCStride;
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
@@ -69,6 +72,7 @@ struct XArgs {
   int nFreq;  // dimX/2+1 for R2C, dimX for C2C
   int ncols;
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
+  long long interZStride, interCStride;  // as YArgs
   const int* colX;
 };
 

@@ -841,7 +841,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return eng.out_at(b, idx - b * n);
   }, [&](int idx, cx<T> v) {
     const int b = idx / n;
-    st_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + idx - b * n], v);
+    st_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + idx - b * n], v);
   });
 }
 
@@ -860,7 +860,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int zl = min(B, a.L - z0);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return ld_inter(&inter[(static_cast<long long>(z0 + b) * a.ncols + c) * a.interStride + pos]);
+    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + pos]);
   };
   if (a.colAddr) {
     // dense entry table: no prologue in front of the row loads
@@ -935,16 +935,16 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int y0 = blockIdx.x * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, n);
-  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  const cx<T>* src = inter + static_cast<long long>(zl) * a.interZStride + y0;
   const int yl = min(B, a.Y - y0);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xcol_of(a, xCol, n - pos);
-      return c < 0 ? czero<T>() : conj(ld_inter(&src[static_cast<long long>(c) * a.interStride + b]));
+      return c < 0 ? czero<T>() : conj(ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]));
     }
     const int c = xcol_of(a, xCol, pos);
-    return c < 0 ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
+    return c < 0 ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, n);
   const int yl = min(B, a.Y - y0);
-  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
     const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
@@ -983,7 +983,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const int c = xcol_of(a, xCol, pos);
-    if (c >= 0 && b < yl) st_inter(&dst[static_cast<long long>(c) * a.interStride + b], v);
+    if (c >= 0 && b < yl) st_inter(&dst[static_cast<long long>(c) * a.interCStride + b], v);
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
@@ -1016,21 +1016,21 @@ __global__ void __launch_bounds__(Eng::kBlock)
   cx<T>* nyq = reinterpret_cast<cx<T>*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   int* xCol = reinterpret_cast<int*>(nyq + B);
   build_xcol(a, xCol, h + 1);
-  const cx<T>* src = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  const cx<T>* src = inter + static_cast<long long>(zl) * a.interZStride + y0;
   const int yl = min(B, a.Y - y0);
   // columns X[0..h] of the block's rows, each element loaded once (lanes run
   // over rows: contiguous column segments)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
     const int k = idx / B, b = idx - k * B;
     const int c = xcol_of(a, xCol, k);
-    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
+    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
   }, [&](int idx) {
     const int k = idx / B;
     return eng.in_at(idx - k * B, k);
   });
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int c = xcol_of(a, xCol, h);
-    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interStride + b]);
+    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
   }
   __syncthreads();
   // pre-pass in place, pairs (k, h-k): Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k
@@ -1073,7 +1073,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const cx<T>* row0 = reinterpret_cast<const cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
   stage_rows(eng, lds, yl, h, [&](int b, int m) { return ld_stream(row0 + static_cast<long long>(b) * h + m); });
   eng.lds_to_lds(lds, twh);
-  cx<T>* dst = inter + static_cast<long long>(zl) * a.ncols * a.interStride + y0;
+  cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
   // post pass: lanes run over rows first, so the column stores are contiguous
   for (int idx = threadIdx.x; idx < B * (h + 1); idx += blockDim.x) {
     const int b = idx % B, k = idx / B;
@@ -1083,7 +1083,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
     const cx<T> e = scale(yk + ym, T(0.5));
     const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
-    st_inter(&dst[static_cast<long long>(c) * a.interStride + b], e + twm<-1>(o, twn[k]));
+    st_inter(&dst[static_cast<long long>(c) * a.interCStride + b], e + twm<-1>(o, twn[k]));
   }
 }
 
