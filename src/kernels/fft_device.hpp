@@ -77,8 +77,9 @@ __host__ __device__ constexpr int padded_stride(int n) {
 
 // Lines per workgroup: as many as fit the LDS budget and the thread cap, with
 // the workgroup a whole number of waves.
-__host__ __device__ constexpr int lines_per_block(int tp, int lineBytes, int budget = kLdsBudget) {
-  int b = kMaxThreads / tp;
+__host__ __device__ constexpr int lines_per_block(int tp, int lineBytes, int budget = kLdsBudget,
+                                                  int maxThreads = kMaxThreads) {
+  int b = maxThreads / tp;
   if (b * lineBytes > budget) b = budget / lineBytes;
   if (b < 1) b = 1;
   if (tp < 64) {
@@ -187,6 +188,47 @@ struct CtShapeSel<double, 128, 1, true> : CtShape128E8 {};
 template <>
 struct CtShapeSel<double, 128, -1, true> : CtShape128E8 {};
 #endif
+// Wide (512-thread) line-fast shapes for the long fp32 / fp64 lines, where the
+// default shapes leave 2 waves per SIMD under the LDS budget. Measured on
+// MI355X (profiles/r2_s1/wide_ab.txt): 512^3 R2C fp32 1400 -> 1438, 512^3 C2C
+// fp64 498 -> 511 transforms/s; for fp32 N = 256 the wide shape was slower
+// (6064 -> 5703 at 256^3 C2C fp32) and stays off.
+#ifndef SPFFT_WIDE_F512
+#define SPFFT_WIDE_F512 1
+#endif
+#ifndef SPFFT_WIDE_D512
+#define SPFFT_WIDE_D512 1
+#endif
+#ifndef SPFFT_WIDE_F256
+#define SPFFT_WIDE_F256 0
+#endif
+#if SPFFT_WIDE_F512
+struct CtShapeF512W {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024, kMaxThr = 512;
+};
+template <>
+struct CtShapeSel<float, 512, 1, true> : CtShapeF512W {};
+template <>
+struct CtShapeSel<float, 512, -1, true> : CtShapeF512W {};
+#endif
+#if SPFFT_WIDE_D512
+struct CtShapeD512W {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8, kBudget = 80 * 1024, kMaxThr = 512;
+};
+template <>
+struct CtShapeSel<double, 512, 1, true> : CtShapeD512W {};
+template <>
+struct CtShapeSel<double, 512, -1, true> : CtShapeD512W {};
+#endif
+#if SPFFT_WIDE_F256
+struct CtShapeF256W {
+  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4, kBudget = kLdsBudget, kMaxThr = 512;
+};
+template <>
+struct CtShapeSel<float, 256, 1, true> : CtShapeF256W {};
+template <>
+struct CtShapeSel<float, 256, -1, true> : CtShapeF256W {};
+#endif
 // (a build with an explicit -DSPFFT_CT256_E=... uses that one shape everywhere)
 #if defined(SPFFT_CT256_DEFAULT_SHAPE)
 template <>
@@ -196,6 +238,17 @@ struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
 #endif
+
+// Workgroup size cap of a shape: Sh::kMaxThr where a shape declares it (wide
+// 512-thread shapes), else kMaxThreads.
+template <class Sh, class = void>
+struct ShapeMaxThreads {
+  static constexpr int value = kMaxThreads;
+};
+template <class Sh>
+struct ShapeMaxThreads<Sh, std::void_t<decltype(Sh::kMaxThr)>> {
+  static constexpr int value = Sh::kMaxThr;
+};
 
 struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 
@@ -240,7 +293,9 @@ struct FftCT {
   static constexpr int E = Sh::E;
   static constexpr int TP = N / E;  // lanes per line
   static constexpr int LS0 = padded_stride<T>(N);
-  static constexpr int B0 = lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), Sh::kBudget);
+  static constexpr int kMaxThr = ShapeMaxThreads<Sh>::value;
+  static constexpr int B0 =
+      lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), Sh::kBudget, kMaxThr);
   static constexpr int B = LF ? lf_lines(B0) : B0;
   static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B) : LS0;
   static constexpr int NT = B * TP;

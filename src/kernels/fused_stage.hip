@@ -377,7 +377,12 @@ bool with_ct_lf(int n, F&& f) {
 }  // namespace
 
 bool fused_supported(int x, int y, int z) {
-  auto ok = [](int n) { return n == 64 || n == 128 || n == 256 || n == 512; };
+  // (the fused kernels are built for workgroups of at most kMaxThreads; the
+  // wide 512-thread shapes of N = 512 are excluded)
+  auto ok = [](int n) {
+    return n == 64 || n == 128 || n == 256 ||
+           (n == 512 && !SPFFT_WIDE_F512 && !SPFFT_WIDE_D512);
+  };
   return ok(x) && ok(y) && ok(z);
 }
 

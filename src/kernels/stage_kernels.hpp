@@ -170,7 +170,7 @@ template <typename T, int N, int S, bool LF = false>
 struct CtEng {
   using F = FftCT<T, N, S, LF>;
   static constexpr bool kBatchedCopy = false;
-  static constexpr int kBlock = kMaxThreads;
+  static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
   __device__ int lines() const { return F::B; }
   __device__ int n() const { return N; }
   __device__ int in_at(int b, int pos) const { return F::in_at(b, pos); }
