@@ -48,6 +48,10 @@ public:
   void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
                  const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
     SPFFT_TIMED_SCOPE("rccl_alltoallv");
+    if (aborted_) {
+      set_error_detail("RCCL: the communicator was aborted after an earlier failure");
+      throw MPIError();
+    }
     const char* s = static_cast<const char*>(send);
     char* r = static_cast<char*>(recv);
     // the local block never leaves the GPU
@@ -68,11 +72,33 @@ public:
   }
   bool host_synchronous() const override { return false; }
   const char* kind() const override { return "rccl"; }
+  bool healthy(std::string* detail) override {
+    if (aborted_) return false;
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(nccl_, &r) != ncclSuccess) return true;  // cannot tell
+    if (r == ncclSuccess || r == ncclInProgress) return true;
+    if (detail) *detail = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
+    return false;
+  }
+  void check() override {
+    std::string d;
+    if (!healthy(&d)) {
+      set_error_detail(d.empty() ? "RCCL: communicator aborted" : d);
+      throw MPIError();
+    }
+  }
+  void abort() override {
+    if (aborted_ || !nccl_) return;
+    aborted_ = true;
+    (void)ncclCommAbort(nccl_);
+    nccl_ = nullptr;
+  }
 
 private:
   std::shared_ptr<Communicator> comm_;
   int rank_, size_;
   ncclComm_t nccl_ = nullptr;
+  bool aborted_ = false;
 };
 
 class LoopbackDeviceComm : public DeviceComm {
@@ -216,16 +242,33 @@ public:
   void complete_writes(hipStream_t stream) override { barrier(stream); }
   void note_read(int slot) override { readPending_[slot & 1] = true; }
   void check() override {
-    if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) != 0) {
-      set_error_detail("peer exchange: a rank did not reach the exchange barrier in time");
+    std::string d;
+    if (!healthy(&d)) {
+      set_error_detail(d);
       throw MPIError();
     }
+  }
+  bool healthy(std::string* detail) override {
+    const unsigned f = __atomic_load_n(failHost_, __ATOMIC_ACQUIRE);
+    if (f == 0) return true;
+    if (detail)
+      *detail = f == kAborted ? "peer exchange: aborted (host-side timeout or an earlier failure)"
+                              : "peer exchange: a rank did not reach the exchange barrier in time";
+    return false;
+  }
+  void abort() override {
+    // the barrier kernels poll this word and stop waiting
+    unsigned expected = 0;
+    __atomic_compare_exchange_n(failHost_, &expected, kAborted, false, __ATOMIC_ACQ_REL,
+                                __ATOMIC_ACQUIRE);
   }
   const char* kind() const override { return ipc_ ? "ipc" : "peer"; }
 
 private:
+  static constexpr unsigned kAborted = 2;
   void barrier(hipStream_t stream) {
     SPFFT_TIMED_SCOPE("peer_barrier");
+    if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) == kAborted) check();
     DeviceGuard guard(device_);
     if (ipc_) {
       dev::launch_peer_barrier(table_->data<unsigned long long*>(),

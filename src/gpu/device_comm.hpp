@@ -20,6 +20,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <string>
 
 #include "spfft/communicator.hpp"
 #include "spfft/types.h"
@@ -59,6 +60,15 @@ public:
   virtual void note_read(int /*slot*/) {}
   // Throws if an asynchronous failure (e.g. a barrier timeout) was recorded.
   virtual void check() {}
+  // Failure detection while the host waits on a stream that carries exchanges:
+  // false (with a description) once the data plane has recorded an
+  // asynchronous error (RCCL: ncclCommGetAsyncError; peer writes: a barrier
+  // that timed out). Cheap enough to poll every millisecond.
+  virtual bool healthy(std::string* /*detail*/) { return true; }
+  // Abandons in-flight communication after a failure or a host-side timeout
+  // (RCCL: ncclCommAbort; peer writes: the barrier kernels stop waiting). The
+  // data plane is unusable afterwards: every later exchange throws MPIError.
+  virtual void abort() {}
   virtual const char* kind() const = 0;
 };
 

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <string>
+#include <thread>
 
 #include "core/timing.hpp"
 #include "fft/fft_plan.hpp"
@@ -420,6 +422,10 @@ void GpuExecutor<T>::synchronize() {
 template <typename T>
 void GpuExecutor<T>::wait_stream() {
   DeviceGuard guard(deviceId_);
+  if (plan_->size > 1) {
+    wait_stream_watched();
+    return;
+  }
   if (gpu_sync_spin()) {
     // poll: wakes within ~1 us of completion instead of the blocking wait's
     // interrupt latency; falls back to the blocking wait after ~20 ms
@@ -432,6 +438,46 @@ void GpuExecutor<T>::wait_stream() {
     }
   }
   gpu_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+// Failure detection for distributed transforms: the
+// host polls the stream and, every millisecond, the data plane's asynchronous
+// error state (RCCL: ncclCommGetAsyncError; peer writes: barrier timeouts). A
+// failure, or a wait longer than SPFFT_COMM_TIMEOUT seconds (0 = no limit, the
+// default), aborts the data plane (ncclCommAbort / barrier kernels released)
+// and throws MPIError with the cause in the error detail, instead of leaving
+// the caller blocked forever on a dead peer.
+template <typename T>
+void GpuExecutor<T>::wait_stream_watched() {
+  DeviceComm& dc = grid_->device_comm();
+  static const double timeout = [] {
+    const char* e = std::getenv("SPFFT_COMM_TIMEOUT");
+    return e && *e ? std::max(0.0, std::atof(e)) : 0.0;
+  }();
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  auto last = t0;
+  for (;;) {
+    const hipError_t e = hipStreamQuery(stream_);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) gpu_check(e, "hipStreamQuery");
+    const auto now = clock::now();
+    if (now - last >= std::chrono::milliseconds(1)) {
+      last = now;
+      std::string detail;
+      const double waited = std::chrono::duration<double>(now - t0).count();
+      if (dc.healthy(&detail) && timeout > 0 && waited > timeout)
+        detail = "exchange did not complete within SPFFT_COMM_TIMEOUT = " + std::to_string(timeout) +
+                 " s";
+      if (!detail.empty()) {
+        dc.abort();
+        set_error_detail(detail + " (data plane aborted)");
+        throw MPIError();
+      }
+    }
+    // spin for the first ~20 ms (low wake-up latency), then yield the core
+    if (now - t0 > std::chrono::milliseconds(20)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 // ------------------------------------------------------------- graph replay

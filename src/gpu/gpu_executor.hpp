@@ -57,6 +57,7 @@ private:
   void build_chunk_plan(int chunks);
   void pipelined_exchange(bool backward);
   void wait_stream();
+  void wait_stream_watched();
   void log_plan() const;
   void poison(bool backward);
   dev::ZArgs zargs() const;

@@ -5,7 +5,8 @@
 // until every rank has reached the epoch. The poll is bounded: after
 // `timeoutTicks` wall-clock ticks the kernel records a failure in a
 // host-mapped word and exits, so a missing peer can never leave a wave
-// spinning on the GPU.
+// spinning on the GPU. A nonzero word (another lane's failure, or an abort
+// written by the host) also ends the wait.
 #include <hip/hip_runtime.h>
 
 #include "kernels/peer_sync.hpp"
@@ -26,6 +27,8 @@ __global__ void __launch_bounds__(64)
   const long long t0 = wall_clock64();
   for (int q = threadIdx.x; q < P; q += blockDim.x) {
     while (__hip_atomic_load(myFlags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      // a failure recorded by another lane, or an abort from the host, ends the wait
+      if (__hip_atomic_load(failure, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
       if (wall_clock64() - t0 > timeoutTicks) {
         __hip_atomic_fetch_or(failure, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;

@@ -91,3 +91,22 @@ def test_bench_driver_launch_2ranks(gpu):
     ndev = torch.cuda.device_count()
     assert rec["config"]["distinct_devices"] == min(2, ndev)
     assert rec["config"]["shared_device"] is (ndev < 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["host-timeout", "peer-timeout"])
+def test_exchange_failure_detected(gpu, mode):
+    """A rank that never joins the exchange: the other rank's call raises MPIError
+    within seconds (data plane aborted) instead of hanging."""
+    probe = os.path.join(REPO, "tools", "failure_probe.py")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", probe, mode]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    line = [l for l in out.splitlines() if l.startswith("DETECTED")]
+    assert line, out[-4000:]
+    seconds = float(line[0].split()[1])
+    assert seconds < 5.0, line[0]
+    assert ("SPFFT_COMM_TIMEOUT" in line[0]) if mode == "host-timeout" else ("barrier" in line[0])
