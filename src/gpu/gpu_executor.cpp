@@ -87,6 +87,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   // profiles/r2_s1/col_table.txt), no change forward
   colTables_ = env_int("SPFFT_COL_TABLE", 0, 0, 1) != 0;
   upload_col_addr(colAddr_, cb);
+  colDescs_ = env_int("SPFFT_COL_DESC", 1, 0, 1) != 0;
+  build_col_desc(colDesc_, cb, layout_.slabStride);
   upload(colX_, p.colX);
   upload(twX_, make_twiddles<T>(p.dimX));
   // packed-real x stage for R2C with even dimX (SPFFT_R2C_PACKED=0 disables)
@@ -170,6 +172,38 @@ void GpuExecutor<T>::upload_col_addr(std::unique_ptr<DeviceBuffer>& buf,
 }
 
 template <typename T>
+void GpuExecutor<T>::build_col_desc(ColDescTable& t, const std::vector<long long>& colBase,
+                                    long long stride) {
+  const IndexPlan& p = *plan_;
+  t.buf.reset();
+  t.stride = stride;
+  if (!colDescs_ || p.num_columns() < 1) return;
+  std::vector<dev::ColDesc> d(p.num_columns());
+  for (int c = 0; c < p.num_columns(); ++c) {
+    dev::ColDesc& q = d[c];
+    for (int r = 0; r < dev::kColRuns; ++r) {
+      q.base[r] = 0;
+      q.y[r] = 0;
+      q.len[r] = 0;
+    }
+    int r = -1;
+    for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e) {
+      const bool extend = r >= 0 && p.colY[e] == q.y[r] + q.len[r] &&
+                          colBase[e] == q.base[r] + static_cast<long long>(q.len[r]) * stride;
+      if (extend) {
+        ++q.len[r];
+        continue;
+      }
+      if (++r >= dev::kColRuns) return;  // too fragmented: LDS-staged entry lists
+      q.base[r] = colBase[e];
+      q.y[r] = p.colY[e];
+      q.len[r] = 1;
+    }
+  }
+  upload(t.buf, d);
+}
+
+template <typename T>
 void GpuExecutor<T>::build_chunk_plan(int K) {
   const IndexPlan& p = *plan_;
   const int P = p.size, me = p.rank;
@@ -212,6 +246,7 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
   for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
   colBaseChunk_.clear();
   colAddrChunk_.clear();
+  colDescChunk_.clear();
   chunks_.assign(K, ChunkXfer{});
   for (int k = 0; k < K; ++k) {
     const i64 lk = pb(me, k + 1) - pb(me, k);
@@ -223,6 +258,8 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
     upload(colBaseChunk_.back(), cb);
     colAddrChunk_.emplace_back();
     upload_col_addr(colAddrChunk_.back(), cb);
+    colDescChunk_.emplace_back();
+    build_col_desc(colDescChunk_.back(), cb, lk);
     ChunkXfer& c = chunks_[k];
     for (int r = 0; r < P; ++r) {
       const int v = k * P + r;
@@ -311,6 +348,7 @@ void GpuExecutor<T>::build_peer_tables() {
     cb[k] = base[p.colRank[k]] + static_cast<i64>(p.colLocal[k]) * layout_.slabStride;
   upload(colBaseRemote_, cb);
   upload_col_addr(colAddrRemote_, cb);
+  build_col_desc(colDescRemote_, cb, layout_.slabStride);
 }
 
 template <typename T>
@@ -652,6 +690,7 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
   a.colAddr = colAddr_ ? colAddr_->data<long long>() : nullptr;
+  set_col_desc(a, colDesc_);
   return a;
 }
 
@@ -800,6 +839,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
       if (ya.L <= ya.zBegin) continue;
       ya.colBase = colBaseChunk_[k]->data<long long>();
       ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
+      set_col_desc(ya, colDescChunk_[k]);
       if (floatExchange_)
         dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
                                              twY_->data<cx<T>>(), stream_);
@@ -883,6 +923,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       if (ya.L > ya.zBegin) {
         ya.colBase = colBaseChunk_[k]->data<long long>();
         ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
+        set_col_desc(ya, colDescChunk_[k]);
         dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
                                  twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
                                  stream_);
@@ -909,6 +950,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     if (peerWrites_) {
       ya.colBase = colBaseRemote_->data<long long>();
       ya.colAddr = colAddrRemote_ ? colAddrRemote_->data<long long>() : nullptr;
+      set_col_desc(ya, colDescRemote_);
       ya.remote = 1;
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,

@@ -108,6 +108,22 @@ private:
   std::unique_ptr<DeviceBuffer> colAddr_, colAddrRemote_;
   std::vector<std::unique_ptr<DeviceBuffer>> colAddrChunk_;
   void upload_col_addr(std::unique_ptr<DeviceBuffer>& buf, const std::vector<long long>& colBase);
+  // per-column run descriptors of the y stage (YArgs::colDesc), one per colBase
+  // table in use; null when some column needs more than kColRuns runs.
+  // SPFFT_COL_DESC=0 disables them.
+  struct ColDescTable {
+    std::unique_ptr<DeviceBuffer> buf;
+    long long stride = 0;
+    const dev::ColDesc* ptr() const { return buf ? buf->data<dev::ColDesc>() : nullptr; }
+  };
+  bool colDescs_ = true;
+  ColDescTable colDesc_, colDescRemote_;
+  std::vector<ColDescTable> colDescChunk_;
+  void build_col_desc(ColDescTable& t, const std::vector<long long>& colBase, long long stride);
+  void set_col_desc(dev::YArgs& a, const ColDescTable& t) const {
+    a.colDesc = t.ptr();
+    a.colStride = t.stride;
+  }
   // peer-write exchange (DeviceComm::peer_writes): the z stage (backward) and y
   // stage (forward) store straight into the receivers' buffers; these tables
   // hold those destinations as element offsets from the local buffer.

@@ -40,6 +40,17 @@ struct ZArgs {
 
 constexpr long long kNoColEntry = -(1LL << 62);
 
+// A column's stick entries as at most kColRuns runs with consecutive y and
+// consecutive bases (base of y = base[r] + (y - y[r]) * YArgs::colStride). A
+// sphere column is two runs (storage y = 0..h and n-h..n-1); entries from
+// several ranks add runs. Workgroup-uniform, so it lives in scalar registers.
+constexpr int kColRuns = 4;
+struct ColDesc {
+  long long base[kColRuns];
+  int y[kColRuns];
+  int len[kColRuns];  // 0 = unused run
+};
+
 struct YArgs {
   int ncols;     // columns of the [z][column][y] intermediate (its row count per plane)
   int colBegin;  // column range processed: [colBegin, colEnd) (exchange pipelining chunks)
@@ -61,6 +72,9 @@ struct YArgs {
   // without staging the column's entry list in LDS (no prologue of dependent
   // loads and barriers before the main loads).
   const long long* colAddr;
+  // optional per-column run descriptors (all columns qualify) and their stride
+  const ColDesc* colDesc;
+  long long colStride;
   int remote;  // forward stores reach peers' memory: release system-wide at exit
 };
 

@@ -737,6 +737,17 @@ inline dim3 y_grid(int cols, int zblocks) {
 }
 
 // ---------------------------------------------------------------- y stage
+// Base of the stick entry at y of a column with a run descriptor, or kNoColEntry.
+__device__ __forceinline__ long long col_desc_base(const ColDesc& d, long long stride, int y) {
+  long long base = kNoColEntry;
+#pragma unroll
+  for (int r = 0; r < kColRuns; ++r) {
+    const unsigned off = static_cast<unsigned>(y - d.y[r]);
+    if (off < static_cast<unsigned>(d.len[r])) base = d.base[r] + static_cast<long long>(off) * stride;
+  }
+  return base;
+}
+
 // y backward through the column's entry list staged in LDS (no dense table,
 // or the x = 0 column of an R2C transform, which needs the hermitian fill).
 // Ends with the FFT result in LDS.
@@ -817,7 +828,22 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
-  if (a.colAddr && c != a.colOfX0) {
+  if (a.colDesc && c != a.colOfX0) {
+    // run descriptor of the column (workgroup-uniform): no prologue, no LDS tables
+    const ColDesc d = a.colDesc[c];
+    auto load = [&](int b, int pos) -> cx<T> {
+      const long long base = col_desc_base(d, a.colStride, pos);
+      if (base == kNoColEntry || b >= zl) return czero<T>();
+      return cvt<T>(ld_stream(&in[base + z0 + b]));
+    };
+    if constexpr (Eng::kBatchedCopy) {
+      eng.stage(lds, load);
+      __syncthreads();
+      eng.lds_to_lds(lds, tw);
+    } else {
+      eng.global_to_lds(lds, tw, load);
+    }
+  } else if (a.colAddr && c != a.colOfX0) {
     // dense entry table: the stick loads start right away
     const long long* ca = a.colAddr + static_cast<long long>(c) * n;
     auto load = [&](int b, int pos) -> cx<T> {
@@ -862,6 +888,21 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (b >= zl) return czero<T>();
     return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + pos]);
   };
+  if (a.colDesc) {
+    const ColDesc d = a.colDesc[c];
+    auto st = [&](int b, int pos, cx<T> v) {
+      const long long base = col_desc_base(d, a.colStride, pos);
+      if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+    };
+#if SPFFT_ROW_STAGE
+    stage_rows(eng, lds, zl, n, load);
+    eng.lds_to_global(lds, tw, st);
+#else
+    eng.global_to_global(lds, tw, load, st);
+#endif
+    release_remote(a.remote);
+    return;
+  }
   if (a.colAddr) {
     // dense entry table: no prologue in front of the row loads
     const long long* ca = a.colAddr + static_cast<long long>(c) * n;
