@@ -83,10 +83,6 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(colY_, p.colY);
   std::vector<long long> cb(layout_.colEntryBase.begin(), layout_.colEntryBase.end());
   upload(colBase_, cb);
-  // opt-in: measured slower for the backward y stage (97 -> 123 us at 256^3,
-  // profiles/r2_s1/col_table.txt), no change forward
-  colTables_ = env_int("SPFFT_COL_TABLE", 0, 0, 1) != 0;
-  upload_col_addr(colAddr_, cb);
   colDescs_ = env_int("SPFFT_COL_DESC", 1, 0, 1) != 0;
   build_col_desc(colDesc_, cb, layout_.slabStride);
   upload(colX_, p.colX);
@@ -151,24 +147,6 @@ void GpuExecutor<T>::log_plan() const {
                twXh_ ? " packed-real" : "", layout_.buffered ? "buffered" : "compact",
                floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, peerWrites_ ? 1 : 0,
                fused_ ? 1 : 0);
-}
-
-template <typename T>
-void GpuExecutor<T>::upload_col_addr(std::unique_ptr<DeviceBuffer>& buf,
-                                     const std::vector<long long>& colBase) {
-  const IndexPlan& p = *plan_;
-  const i64 elems = static_cast<i64>(p.num_columns()) * p.dimY;
-  // 8 bytes per (column, y): 512 KB at 256^3, 2 MB at 512^3; very large grids
-  // keep the LDS-staged entry lists
-  if (!colTables_ || elems < 1 || elems > (i64(1) << 23)) {
-    buf.reset();
-    return;
-  }
-  std::vector<long long> t(static_cast<std::size_t>(elems), dev::kNoColEntry);
-  for (int c = 0; c < p.num_columns(); ++c)
-    for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e)
-      t[static_cast<std::size_t>(c) * p.dimY + p.colY[e]] = colBase[e];
-  upload(buf, t);
 }
 
 template <typename T>
@@ -245,7 +223,6 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
   planeBounds_.resize(K + 1);
   for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
   colBaseChunk_.clear();
-  colAddrChunk_.clear();
   colDescChunk_.clear();
   chunks_.assign(K, ChunkXfer{});
   for (int k = 0; k < K; ++k) {
@@ -256,8 +233,6 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
       cb[e] = slabDispl[k * P + p.colRank[e]] + static_cast<i64>(p.colLocal[e]) * lk - pb(me, k);
     colBaseChunk_.emplace_back();
     upload(colBaseChunk_.back(), cb);
-    colAddrChunk_.emplace_back();
-    upload_col_addr(colAddrChunk_.back(), cb);
     colDescChunk_.emplace_back();
     build_col_desc(colDescChunk_.back(), cb, lk);
     ChunkXfer& c = chunks_[k];
@@ -347,7 +322,6 @@ void GpuExecutor<T>::build_peer_tables() {
   for (std::size_t k = 0; k < p.colY.size(); ++k)
     cb[k] = base[p.colRank[k]] + static_cast<i64>(p.colLocal[k]) * layout_.slabStride;
   upload(colBaseRemote_, cb);
-  upload_col_addr(colAddrRemote_, cb);
   build_col_desc(colDescRemote_, cb, layout_.slabStride);
 }
 
@@ -689,7 +663,6 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
-  a.colAddr = colAddr_ ? colAddr_->data<long long>() : nullptr;
   set_col_desc(a, colDesc_);
   return a;
 }
@@ -838,7 +811,6 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L <= ya.zBegin) continue;
       ya.colBase = colBaseChunk_[k]->data<long long>();
-      ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
       set_col_desc(ya, colDescChunk_[k]);
       if (floatExchange_)
         dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
@@ -922,7 +894,6 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L > ya.zBegin) {
         ya.colBase = colBaseChunk_[k]->data<long long>();
-        ya.colAddr = colAddrChunk_[k] ? colAddrChunk_[k]->data<long long>() : nullptr;
         set_col_desc(ya, colDescChunk_[k]);
         dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
                                  twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
@@ -949,7 +920,6 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
         interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (peerWrites_) {
       ya.colBase = colBaseRemote_->data<long long>();
-      ya.colAddr = colAddrRemote_ ? colAddrRemote_->data<long long>() : nullptr;
       set_col_desc(ya, colDescRemote_);
       ya.remote = 1;
     }

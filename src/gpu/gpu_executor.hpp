@@ -102,12 +102,6 @@ private:
   // device tables
   std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_, zRank_, segDispl_, segStride_, segZOff_;
   std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
-  // dense [ncols][dimY] entry-base tables of the y stage (YArgs::colAddr), one
-  // per colBase table in use; opt-in with SPFFT_COL_TABLE=1 (measured slower)
-  bool colTables_ = false;
-  std::unique_ptr<DeviceBuffer> colAddr_, colAddrRemote_;
-  std::vector<std::unique_ptr<DeviceBuffer>> colAddrChunk_;
-  void upload_col_addr(std::unique_ptr<DeviceBuffer>& buf, const std::vector<long long>& colBase);
   // per-column run descriptors of the y stage (YArgs::colDesc), one per colBase
   // table in use; null when some column needs more than kColRuns runs.
   // SPFFT_COL_DESC=0 disables them.

@@ -38,6 +38,8 @@ struct ZArgs {
   int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
 };
 
+// "no stick at this y" marker of a column lookup (bases of the peer-write
+// tables are offsets to other GPUs' buffers and may be negative)
 constexpr long long kNoColEntry = -(1LL << 62);
 
 // A column's stick entries as at most kColRuns runs with consecutive y and
@@ -66,12 +68,6 @@ struct YArgs {
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
-  // optional dense [ncols][n] table: colBase of the entry at (column, y),
-  // kNoColEntry where the column has no stick at y (bases of the peer-write
-  // tables are offsets to other GPUs' buffers and may be negative). Lets a workgroup address its sticks
-  // without staging the column's entry list in LDS (no prologue of dependent
-  // loads and barriers before the main loads).
-  const long long* colAddr;
   // optional per-column run descriptors (all columns qualify) and their stride
   const ColDesc* colDesc;
   long long colStride;

@@ -843,21 +843,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     } else {
       eng.global_to_lds(lds, tw, load);
     }
-  } else if (a.colAddr && c != a.colOfX0) {
-    // dense entry table: the stick loads start right away
-    const long long* ca = a.colAddr + static_cast<long long>(c) * n;
-    auto load = [&](int b, int pos) -> cx<T> {
-      const long long base = ca[pos];
-      if (base == kNoColEntry || b >= zl) return czero<T>();
-      return cvt<T>(ld_stream(&in[base + z0 + b]));
-    };
-    if constexpr (Eng::kBatchedCopy) {
-      eng.stage(lds, load);
-      __syncthreads();
-      eng.lds_to_lds(lds, tw);
-    } else {
-      eng.global_to_lds(lds, tw, load);
-    }
   } else {
     y_backward_entries(eng, a, in, tw, lds, c, z0, zl);
   }
@@ -892,22 +877,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const ColDesc d = a.colDesc[c];
     auto st = [&](int b, int pos, cx<T> v) {
       const long long base = col_desc_base(d, a.colStride, pos);
-      if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
-    };
-#if SPFFT_ROW_STAGE
-    stage_rows(eng, lds, zl, n, load);
-    eng.lds_to_global(lds, tw, st);
-#else
-    eng.global_to_global(lds, tw, load, st);
-#endif
-    release_remote(a.remote);
-    return;
-  }
-  if (a.colAddr) {
-    // dense entry table: no prologue in front of the row loads
-    const long long* ca = a.colAddr + static_cast<long long>(c) * n;
-    auto st = [&](int b, int pos, cx<T> v) {
-      const long long base = ca[pos];
       if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
     };
 #if SPFFT_ROW_STAGE
