@@ -280,12 +280,15 @@ def test_user_stream_async(gpu):
     assert (out - vals).abs().max().item() < 1e-12
 
 
-@pytest.mark.parametrize("chunks", [1, 3, 8])
+@pytest.mark.parametrize("chunks,exchange", [(1, "COMPACT_BUFFERED"), (3, "COMPACT_BUFFERED"),
+                                             (8, "COMPACT_BUFFERED"),
+                                             (3, "COMPACT_BUFFERED_FLOAT"), (3, "BUFFERED")])
 @pytest.mark.parametrize("dist", ["uniform", "rank0", "rank0_planes_last", "r2c"])
-def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, monkeypatch):
+def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, exchange, monkeypatch):
     """Reference distribution sweep (tests/mpi_tests/test_transform.cpp) on P=3 virtual
-    ranks of one GPU, through the pipelined exchange with 1, 3 and 8 chunks (ranks
-    with few or no sticks get empty chunks; every rank issues the same rounds)."""
+    ranks of one GPU, through the plane-chunk pipelined exchange with 1, 3 and 8 chunks
+    (ranks with few or no planes get empty chunks; every rank issues the same rounds),
+    also with fp32 exchange buffers and the padded BUFFERED layout (never chunked)."""
     import torch
     from spfft_amd.parallel import run_ranks
     from spfft_amd.utils.indices import calculate_num_local_xy_planes
@@ -318,7 +321,7 @@ def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, monkeypatch):
     def body(rank, comm):
         torch.cuda.set_device(0)
         grid = sp.Grid(nx, ny, nz, max(1, max_sticks), GPU, 1, max_local_z_length=max(planes),
-                       comm=comm, exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+                       comm=comm, exchange_type=getattr(sp.ExchangeType, exchange))
         t = grid.create_transform(GPU, ttype, nx, ny, nz, planes[rank], parts[rank])
         v = torch.as_tensor(vals_all[starts[rank]:starts[rank + 1]], device="cuda")
         errs = []
@@ -333,8 +336,9 @@ def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, monkeypatch):
         errs.append(max_rel_error(f, ref_fwd[starts[rank]:starts[rank + 1]]) if len(f) else 0.0)
         return max(errs)
 
+    tol = 1e-5 if exchange.endswith("FLOAT") else 1e-11
     for e in run_ranks(P, body):
-        assert e < 1e-11
+        assert e < tol
 
 
 @pytest.mark.parametrize("dims,ttype", [((16, 12, 20), "c2c"), ((11, 13, 12), "c2c"),
