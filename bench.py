@@ -211,6 +211,9 @@ def main():
     # no measured reference exists for other configs or for N > 1 GPUs
     headline = (n == 256 and a.cutoff == 0.5 and a.type == "c2c" and not single)
     vs_baseline = rate / REF_FFT_ONLY_256 if (headline and world == 1) else None
+    if a.timing:
+        for tr in ts:  # completes the GPU stage intervals (gpu/<direction>/<stage>)
+            tr.synchronize()
     if rank == 0:
         if a.timing:
             print(sp.timing_report(), file=sys.stderr)

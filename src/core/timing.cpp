@@ -167,6 +167,23 @@ std::string report_text() {
   return os.str();
 }
 
+void add_sample(std::initializer_list<const char*> path, double seconds) {
+  if (!enabled()) return;
+  auto& r = registry();
+  std::lock_guard<std::mutex> lock(r.mutex);
+  Node* n = &r.root;
+  for (const char* name : path) {
+    auto& slot = n->children[name];
+    if (!slot) {
+      slot.reset(new Node());
+      slot->name = name;
+      slot->parent = n;
+    }
+    n = slot.get();
+  }
+  n->samples.push_back(seconds);
+}
+
 Scope::Scope(const char* name) {
   auto& rx = roctx();
   if (rx.push) {

@@ -7,6 +7,7 @@
 // every scope emits a roctx range (visible with rocprofv3 --marker-trace).
 #pragma once
 
+#include <initializer_list>
 #include <string>
 
 namespace spfft {
@@ -17,6 +18,9 @@ void set_enabled(bool on);
 void reset();
 std::string report_json();
 std::string report_text();
+// Adds one sample (seconds) to the node root/path[0]/path[1]/... (GPU-side
+// stage times measured with hipEvents, which are known only after the fact).
+void add_sample(std::initializer_list<const char*> path, double seconds);
 
 class Scope {
 public:

@@ -426,6 +426,7 @@ void GpuExecutor<T>::reset_stream() {
 template <typename T>
 void GpuExecutor<T>::synchronize() {
   wait_stream();
+  if (!traces_.empty()) harvest_stage_times(false);
   // a peer barrier that timed out leaves a flag behind (data are incomplete)
   if (peerWrites_) grid_->device_comm().check();
   check_fused();
@@ -450,6 +451,56 @@ void GpuExecutor<T>::wait_stream() {
     }
   }
   gpu_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+// ---------------------------------------------------------- stage timing
+template <typename T>
+void GpuExecutor<T>::stage_mark(const char* dir, const char* stage) {
+  if (!timing::enabled() || capturing_) return;
+  if (!stage) {
+    // a direction starts: collect what has completed, bound the backlog
+    harvest_stage_times(traces_.size() >= 64);
+    traces_.push_back(StageTrace{dir, {}});
+  }
+  if (traces_.empty() || traces_.back().dir != dir) return;
+  StageMark m;
+  if (!spareEvents_.empty()) {
+    m.ev = std::move(spareEvents_.back());
+    spareEvents_.pop_back();
+  } else {
+    m.ev.reset(new GpuEvent(true));
+  }
+  m.ev->record(stream_);
+  m.stage = stage;
+  traces_.back().marks.push_back(std::move(m));
+}
+
+template <typename T>
+void GpuExecutor<T>::harvest_stage_times(bool wait) {
+  std::size_t done = 0;
+  for (auto& t : traces_) {
+    if (t.marks.empty()) {
+      ++done;
+      continue;
+    }
+    hipEvent_t last = t.marks.back().ev->get();
+    if (wait) {
+      gpu_check(hipEventSynchronize(last), "hipEventSynchronize");
+    } else {
+      const hipError_t e = hipEventQuery(last);
+      if (e == hipErrorNotReady) break;
+      gpu_check(e, "hipEventQuery");
+    }
+    for (std::size_t i = 1; i < t.marks.size(); ++i) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, t.marks[i - 1].ev->get(), t.marks[i].ev->get()) == hipSuccess)
+        timing::add_sample({"gpu", t.dir, t.marks[i].stage}, 1e-3 * ms);
+    }
+    for (auto& m : t.marks) spareEvents_.push_back(std::move(m.ev));
+    ++done;
+  }
+  traces_.erase(traces_.begin(), traces_.begin() + static_cast<std::ptrdiff_t>(done));
+  (void)hipGetLastError();
 }
 
 // Failure detection for distributed transforms: the
@@ -712,6 +763,8 @@ void GpuExecutor<T>::backward_z(const T* input) {
   SPFFT_TIMED_SCOPE("gpu_backward_z");
   DeviceGuard guard(deviceId_);
   order_after_default_stream();
+  stage_mark("backward", nullptr);
+  StageEnd stageEnd{this, "backward", "z"};
   poison(true);
   const IndexPlan& p = *plan_;
   const cx<T>* values = reinterpret_cast<const cx<T>*>(input);
@@ -765,6 +818,7 @@ void GpuExecutor<T>::exchange(bool backward) {
 template <typename T>
 void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_backward_exchange");
+  StageEnd stageEnd{this, "backward", "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
@@ -783,6 +837,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   if (outputLocation != SPFFT_PU_HOST && outputLocation != SPFFT_PU_GPU)
     throw InvalidParameterError();
   DeviceGuard guard(deviceId_);
+  StageEnd stageEnd{this, "backward", "y+x"};
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   auto* interBase = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
@@ -865,6 +920,8 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     throw InvalidParameterError();
   DeviceGuard guard(deviceId_);
   order_after_default_stream();
+  stage_mark("forward", nullptr);
+  StageEnd stageEnd{this, "forward", "x+y"};
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (inputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(space, grid_->host_slot(GridImpl<T>::kSpace), space_bytes(),
@@ -937,6 +994,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
 template <typename T>
 void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_forward_exchange");
+  StageEnd stageEnd{this, "forward", "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
@@ -953,6 +1011,7 @@ template <typename T>
 void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   SPFFT_TIMED_SCOPE("gpu_forward_z");
   DeviceGuard guard(deviceId_);
+  StageEnd stageEnd{this, "forward", "z"};
   const IndexPlan& p = *plan_;
   const T factor =
       scaling == SPFFT_FULL_SCALING

@@ -152,6 +152,34 @@ private:
   std::unique_ptr<GpuStream> commStream_;
   std::vector<std::unique_ptr<GpuEvent>> chunkEvents_;
   std::unique_ptr<GpuEvent> commDone_, zDone_;
+  // GPU-side stage timing (SPFFT_TIMING=1): timing events recorded on the
+  // execution stream at the stage boundaries of each direction; the intervals
+  // go into the timing tree as gpu/<direction>/<stage> once they completed.
+  struct StageMark {
+    std::unique_ptr<GpuEvent> ev;
+    const char* stage;  // stage that ends at this mark (nullptr: direction start)
+  };
+  struct StageTrace {
+    const char* dir;
+    std::vector<StageMark> marks;
+  };
+  std::vector<StageTrace> traces_;
+  std::vector<std::unique_ptr<GpuEvent>> spareEvents_;
+  void stage_mark(const char* dir, const char* stage);
+  // records the end mark of a stage when the stage function returns
+  struct StageEnd {
+    GpuExecutor* e;
+    const char* dir;
+    const char* stage;
+    ~StageEnd() {
+      try {
+        e->stage_mark(dir, stage);
+      } catch (...) {
+      }
+    }
+  };
+  void harvest_stage_times(bool wait);
+
   std::unique_ptr<DeviceBuffer> twX_, twXh_, twY_, twZ_;
   std::unique_ptr<DeviceBuffer> staging_;
   std::vector<std::int64_t> bwdSendCounts_, bwdSendDispls_, bwdRecvCounts_, bwdRecvDispls_;

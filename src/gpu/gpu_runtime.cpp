@@ -85,7 +85,10 @@ GpuStream::~GpuStream() {
   if (stream_ && !process_exiting()) (void)hipStreamDestroy(stream_);
 }
 
-GpuEvent::GpuEvent() { gpu_check(hipEventCreateWithFlags(&event_, hipEventDisableTiming), "hipEventCreate"); }
+GpuEvent::GpuEvent(bool timing) {
+  gpu_check(hipEventCreateWithFlags(&event_, timing ? hipEventDefault : hipEventDisableTiming),
+            "hipEventCreate");
+}
 GpuEvent::~GpuEvent() {
   if (event_ && !process_exiting()) (void)hipEventDestroy(event_);
 }

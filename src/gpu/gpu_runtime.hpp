@@ -55,7 +55,7 @@ private:
 
 class GpuEvent {
 public:
-  GpuEvent();  // timing disabled
+  explicit GpuEvent(bool timing = false);  // timing disabled unless asked for
   ~GpuEvent();
   GpuEvent(const GpuEvent&) = delete;
   GpuEvent& operator=(const GpuEvent&) = delete;

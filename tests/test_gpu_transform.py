@@ -463,3 +463,37 @@ def test_graph_replay(gpu, ttype, monkeypatch):
     finally:
         sp.timing_enable(False)
     assert "gpu_backward_graph" in report and "gpu_forward_graph" in report, report
+
+
+def test_gpu_stage_timing(gpu):
+    """SPFFT_TIMING: hipEvent intervals of every stage land in the timing tree
+    (gpu/<direction>/<stage>) once the calls completed; SURVEY.md section 5."""
+    import torch
+    rng = np.random.default_rng(31)
+    dims = (64, 64, 64)
+    idx = sphere_indices(*dims, 0.5)
+    grid = sp.Grid(*dims, 64 * 64, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.C2C, *dims, 64, idx)
+    vals = torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu)
+    sp.timing_reset()
+    sp.timing_enable(True)
+    try:
+        for _ in range(3):
+            t.backward(vals)
+            t.forward(None, scaling=sp.Scaling.FULL)
+        t.synchronize()
+        tree = sp.timing_json()
+    finally:
+        sp.timing_enable(False)
+    gpu_node = [n for n in tree["timings"] if n["identifier"] == "gpu"]
+    assert gpu_node, tree
+    dirs = {d["identifier"]: {s["identifier"]: s for s in d["sub-timings"]}
+            for d in gpu_node[0]["sub-timings"]}
+    assert set(dirs) == {"backward", "forward"}, dirs
+    for d, stages in (("backward", ("z", "exchange", "y+x")), ("forward", ("x+y", "exchange", "z"))):
+        for st in stages:
+            node = dirs[d][st]
+            assert node["count"] == 3, (d, st, node)
+            assert node["min"] >= 0.0
+        # the FFT stages of a 64^3 transform take measurable GPU time
+        assert dirs[d]["z"]["total"] > 0.0
