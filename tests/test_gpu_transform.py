@@ -497,3 +497,44 @@ def test_gpu_stage_timing(gpu):
             assert node["min"] >= 0.0
         # the FFT stages of a 64^3 transform take measurable GPU time
         assert dirs[d]["z"]["total"] > 0.0
+
+
+def test_reference_size_sweep_full(gpu):
+    """The reference's complete local sweep on the GPU: X, Y, Z in {1, 2, 11, 12, 13, 100}
+    (all 216 combinations; tests/local_tests/test_local_transform.cpp), C2C with and
+    without centred indices (run twice: zero-fill), forward with full scaling, and R2C
+    forward/backward against numpy."""
+    import itertools
+
+    import torch
+    sizes = [1, 2, 11, 12, 13, 100]
+    rng = np.random.default_rng(216)
+    failures = []
+    for n, dims in enumerate(itertools.product(sizes, sizes, sizes)):
+        nx, ny, nz = dims
+        centered = n % 2 == 1
+        idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+        if centered:
+            idx = center_indices(dims, [idx])[0]
+        vals = _rand_vals(rng, len(idx))
+        grid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+        t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+        ref = dense_backward(idx, vals, dims)
+        dv = torch.as_tensor(vals, device=gpu)
+        errs = [max_rel_error(t.backward(dv).cpu().numpy(), ref) for _ in range(2)]
+        space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+        f = t.forward(torch.as_tensor(space, device=gpu), scaling=sp.Scaling.FULL)
+        errs.append(max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims, scale=True)))
+        # R2C on the same grid shape (hermitian half of the indices)
+        ridx = create_value_indices(rng, [1.0], 1.0, 1.0, nx, ny, nz, True)[0]
+        rgrid = sp.Grid(nx, ny, nz, nx * ny, GPU, 1)
+        rt = rgrid.create_transform(GPU, sp.TransformType.R2C, nx, ny, nz, nz, ridx)
+        rspace = rng.standard_normal((nz, ny, nx))
+        rf = rt.forward(torch.as_tensor(rspace, device=gpu))
+        errs.append(max_rel_error(rf.cpu().numpy(), dense_forward(rspace, ridx, dims)))
+        rb = rt.backward(rf)
+        errs.append(max_rel_error(rb.cpu().numpy(), dense_backward(ridx, rf.cpu().numpy(), dims,
+                                                                   r2c=True)))
+        if max(errs) > 1e-11:
+            failures.append((dims, centered, errs))
+    assert not failures, failures[:5]

@@ -105,3 +105,27 @@ def test_large_prime_bluestein(dims, r2c):
     assert max_rel_error(out, dense_backward(idx, vals, dims, r2c=r2c)) < 1e-12
     f = np.array(t.forward(space))
     assert max_rel_error(f, vals) < 1e-12
+
+
+def test_reference_size_sweep_full():
+    """All 216 combinations of the reference sweep on the host engine in one loop
+    (C2C alternating centred indices, run twice, scaled forward)."""
+    rng = np.random.default_rng(216)
+    failures = []
+    for n, dims in enumerate(itertools.product(SIZES, SIZES, SIZES)):
+        nx, ny, nz = dims
+        idx = create_value_indices(rng, [1.0], 0.7, 0.7, nx, ny, nz, False)[0]
+        centered = n % 2 == 1
+        if centered:
+            idx = center_indices(dims, [idx])[0]
+        vals = rng.standard_normal(len(idx)) + 1j * rng.standard_normal(len(idx))
+        grid = sp.Grid(nx, ny, nz, nx * ny, HOST, 4)
+        t = grid.create_transform(HOST, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+        ref = dense_backward(idx, vals, dims)
+        errs = [max_rel_error(t.backward(vals), ref) for _ in range(2)]
+        space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+        errs.append(max_rel_error(t.forward(space, scaling=sp.Scaling.FULL),
+                                  dense_forward(space, idx, dims, scale=True)))
+        if max(errs) > 1e-11:
+            failures.append((dims, centered, errs))
+    assert not failures, failures[:5]
