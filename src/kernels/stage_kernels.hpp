@@ -968,6 +968,13 @@ __device__ __forceinline__ int xcol_of(const XArgs& a, const int* xCol, int x) {
   return x_dense(a) ? (x < a.nFreq ? x : -1) : xCol[x];
 }
 
+// Packed-real C2R with the pre-pass folded into the first FFT pass's loads
+// (compile-time engines): 66.9 -> 54.8 us at 256^3 fp64, R2C bench +2% fp64,
+// +3% fp32 (profiles/r2_s1/shape_ab.txt). 0 restores the LDS-staged pre-pass.
+#ifndef SPFFT_C2R_DIRECT
+#define SPFFT_C2R_DIRECT 1
+#endif
+
 // ---------------------------------------------------------------- x stage
 // Backward x stage with the line-fast engine: lane (line = row y, pos = x)
 // reads column x of the intermediate (consecutive lanes -> consecutive y),
@@ -1073,6 +1080,33 @@ __global__ void __launch_bounds__(Eng::kBlock)
   build_xcol(a, xCol, h + 1);
   const cx<T>* src = inter + static_cast<long long>(zl) * a.interZStride + y0;
   const int yl = min(B, a.Y - y0);
+#if SPFFT_C2R_DIRECT
+  if constexpr (!Eng::kBatchedCopy) {
+    // pre-pass folded into the FFT's first-pass loads: the lane that needs Z[k]
+    // loads X[k] and X[h-k] itself (the mirror column is the same workgroup's
+    // data, so its second read is served by the caches; plain loads keep it there)
+    auto col = [&](int k, int b) -> cx<T> {
+      const int c = xcol_of(a, xCol, k);
+      return (c < 0 || b >= yl) ? czero<T>() : src[static_cast<long long>(c) * a.interCStride + b];
+    };
+    eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
+      cx<T> xk = col(k, b);
+      cx<T> xm = col(h - k, b);
+      if (k == 0) {
+        xk.y = T(0);
+        xm.y = T(0);
+      }
+      const cx<T> xmc = conj(xm);
+      return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twn[k]));
+    });
+    cx<T>* out = reinterpret_cast<cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
+    copy_out<Eng>(lds, yl * h, [&](int idx) {
+      const int b = idx / h;
+      return eng.out_at(b, idx - b * h);
+    }, [&](int idx, cx<T> v) { st_stream(&out[idx], v); });
+    return;
+  }
+#endif
   // columns X[0..h] of the block's rows, each element loaded once (lanes run
   // over rows: contiguous column segments)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
