@@ -170,6 +170,7 @@ template <typename T, int N, int S, bool LF = false>
 struct CtEng {
   using F = FftCT<T, N, S, LF>;
   static constexpr bool kBatchedCopy = false;
+  static constexpr bool kLineFast = LF;
   static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
   __device__ int lines() const { return F::B; }
   __device__ int n() const { return N; }
@@ -205,6 +206,7 @@ struct CtEng {
 template <typename T, int S, bool LF = false>
 struct RtEng {
   static constexpr bool kBatchedCopy = true;
+  static constexpr bool kLineFast = LF;
   static constexpr int kBlock = kRtThreads;
   RtPlan p;
   __device__ int lines() const { return p.lines; }
@@ -285,6 +287,7 @@ struct RtEng {
 template <typename T, int S>
 struct BlueEng {
   static constexpr bool kBatchedCopy = true;
+  static constexpr bool kLineFast = false;
   static constexpr int kBlock = kMaxThreads;
   RtPlan pm;  // length m, ls = m
   int nn;
@@ -1162,8 +1165,17 @@ __global__ void __launch_bounds__(Eng::kBlock)
   build_xcol(a, xCol, h + 1);
   const int yl = min(B, a.Y - y0);
   const cx<T>* row0 = reinterpret_cast<const cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
-  stage_rows(eng, lds, yl, h, [&](int b, int m) { return ld_stream(row0 + static_cast<long long>(b) * h + m); });
-  eng.lds_to_lds(lds, twh);
+  auto rowLoad = [&](int b, int m) -> cx<T> {
+    return b >= yl ? czero<T>() : ld_stream(row0 + static_cast<long long>(b) * h + m);
+  };
+  if constexpr (!Eng::kBatchedCopy && !Eng::kLineFast) {
+    // row-mapped engine (SPFFT_R2C_ROWMAP): a line's lanes are adjacent, so the
+    // first pass loads the real rows straight from global memory
+    eng.global_to_lds(lds, twh, rowLoad);
+  } else {
+    stage_rows(eng, lds, yl, h, rowLoad);
+    eng.lds_to_lds(lds, twh);
+  }
   cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
   // post pass: lanes run over rows first, so the column stores are contiguous
   for (int idx = threadIdx.x; idx < B * (h + 1); idx += blockDim.x) {
