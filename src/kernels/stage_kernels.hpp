@@ -790,71 +790,52 @@ __device__ __forceinline__ long long col_desc_base(const ColDesc& d, long long s
   return base;
 }
 
-// y backward through the column's entry list staged in LDS (no dense table,
-// or the x = 0 column of an R2C transform, which needs the hermitian fill).
-// Ends with the FFT result in LDS.
-template <class Eng, typename T, typename BT>
-__device__ void y_backward_entries(const Eng& eng, const YArgs& a, const BT* __restrict__ in,
-                                   const cx<T>* __restrict__ tw, cx<T>* lds, int c, int z0, int zl) {
-  const int B = eng.lines();
-  const int n = eng.n();
-  const int k0 = a.colOffsets[c];
-  const int ne = a.colOffsets[c + 1] - k0;
-  long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  int* yEnt = reinterpret_cast<int*>(cBase + n);
-  int* cY = yEnt + n;
-  for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
-  __syncthreads();
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    const int y = a.colY[k0 + e];
-    cBase[e] = a.colBase[k0 + e] + z0;
-    yEnt[y] = e;
-    cY[e] = y;
-  }
-  __syncthreads();
-  auto load = [&](int b, int pos) -> cx<T> {
-    const int e = yEnt[pos];
-    if (e < 0 || b >= zl) return czero<T>();
-    return cvt<T>(ld_stream(&in[cBase[e] + b]));
-  };
-  if constexpr (Eng::kBatchedCopy) {
-    // run-time engines: stage either input path, then one FFT (a single inlined
-    // copy of the pass switch keeps the kernel's register demand down)
-    if (c != a.colOfX0) {
-      eng.stage(lds, load);
-      __syncthreads();
-    } else {
-      zero_lds(lds, eng.input_elems());
-      __syncthreads();
-      gather_to_lds(lds, ne * zl, [&](int idx) {
-        const int e = idx / zl, zz = idx - e * zl;
-        return cvt<T>(ld_stream(&in[cBase[e] + zz]));
-      }, [&](int idx) {
-        const int e = idx / zl, zz = idx - e * zl;
-        return eng.in_at(zz, cY[e]);
-      });
-      __syncthreads();
-      hermitian_lines(eng, lds, 0, B, n);
+// Stick entries of the workgroup's column: through the column's run descriptor
+// (workgroup-uniform, scalar registers, no prologue) when the plan has one, else
+// through the entry list staged in LDS (colBase per entry, y -> entry table).
+// Every kernel keeps a single FFT call site whichever source is used: the
+// run-time engines inline their whole pass switch per call site, and a second
+// copy doubled their register demand (profiles/r2_s1/rt_regression.txt).
+template <class Eng>
+struct ColEntries {
+  bool useDesc;
+  ColDesc d;
+  long long stride;
+  long long* cBase;  // LDS: colBase per entry (list mode)
+  int* yEnt;         // LDS: y -> entry or -1 (list mode)
+  int* cY;           // LDS: entry -> y (list mode)
+  int ne;
+  __device__ ColEntries(const Eng& eng, const YArgs& a, cx<double>* ldsBase, int c, bool allowDesc) {
+    const int n = eng.n();
+    useDesc = allowDesc && a.colDesc != nullptr;
+    stride = a.colStride;
+    cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(ldsBase) + eng.lds_bytes());
+    yEnt = reinterpret_cast<int*>(cBase + n);
+    cY = yEnt + n;
+    ne = 0;
+    if (useDesc) {
+      d = a.colDesc[c];
+      return;
     }
-    eng.lds_to_lds(lds, tw);
-  } else if (c != a.colOfX0) {
-    eng.global_to_lds(lds, tw, load);
-  } else {
-    zero_lds(lds, eng.input_elems());
+    const int k0 = a.colOffsets[c];
+    ne = a.colOffsets[c + 1] - k0;
+    for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
     __syncthreads();
-    gather_to_lds(lds, ne * zl, [&](int idx) {
-      const int e = idx / zl, zz = idx - e * zl;
-      return cvt<T>(ld_stream(&in[cBase[e] + zz]));
-    }, [&](int idx) {
-      const int e = idx / zl, zz = idx - e * zl;
-      return eng.in_at(zz, cY[e]);
-    });
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+      const int y = a.colY[k0 + e];
+      cBase[e] = a.colBase[k0 + e];
+      yEnt[y] = e;
+      cY[e] = y;
+    }
     __syncthreads();
-    hermitian_lines(eng, lds, 0, B, n);
-    eng.lds_to_lds(lds, tw);
   }
-}
-
+  // base of the entry at y (add the plane), or kNoColEntry
+  __device__ long long base(int y) const {
+    if (useDesc) return col_desc_base(d, stride, y);
+    const int e = yEnt[y];
+    return e < 0 ? kNoColEntry : cBase[e];
+  }
+};
 
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
 // loads straight from the stick side — consecutive lanes read consecutive z
@@ -870,23 +851,41 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
-  if (a.colDesc && c != a.colOfX0) {
-    // run descriptor of the column (workgroup-uniform): no prologue, no LDS tables
-    const ColDesc d = a.colDesc[c];
-    auto load = [&](int b, int pos) -> cx<T> {
-      const long long base = col_desc_base(d, a.colStride, pos);
-      if (base == kNoColEntry || b >= zl) return czero<T>();
-      return cvt<T>(ld_stream(&in[base + z0 + b]));
-    };
-    if constexpr (Eng::kBatchedCopy) {
+  const bool x0 = c == a.colOfX0;
+  const ColEntries<Eng> ce(eng, a, reinterpret_cast<cx<double>*>(lds), c, !x0);
+  auto load = [&](int b, int pos) -> cx<T> {
+    const long long base = ce.base(pos);
+    if (base == kNoColEntry || b >= zl) return czero<T>();
+    return cvt<T>(ld_stream(&in[base + z0 + b]));
+  };
+  // the x = 0 column of an R2C transform: gathered into LDS, hermitian fill
+  auto stage_x0 = [&]() {
+    zero_lds(lds, eng.input_elems());
+    __syncthreads();
+    gather_to_lds(lds, ce.ne * zl, [&](int idx) {
+      const int e = idx / zl, zz = idx - e * zl;
+      return cvt<T>(ld_stream(&in[ce.cBase[e] + z0 + zz]));
+    }, [&](int idx) {
+      const int e = idx / zl, zz = idx - e * zl;
+      return eng.in_at(zz, ce.cY[e]);
+    });
+    __syncthreads();
+    hermitian_lines(eng, lds, 0, B, n);
+  };
+  if constexpr (Eng::kBatchedCopy) {
+    // run-time engines: stage either input path, then one FFT
+    if (!x0) {
       eng.stage(lds, load);
       __syncthreads();
-      eng.lds_to_lds(lds, tw);
     } else {
-      eng.global_to_lds(lds, tw, load);
+      stage_x0();
     }
+    eng.lds_to_lds(lds, tw);
+  } else if (!x0) {
+    eng.global_to_lds(lds, tw, load);
   } else {
-    y_backward_entries(eng, a, in, tw, lds, c, z0, zl);
+    stage_x0();
+    eng.lds_to_lds(lds, tw);
   }
   // rows of [z][column][y] are contiguous: coalesced copy-out
   copy_out<Eng>(lds, zl * n, [&](int idx) {
@@ -911,39 +910,14 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
+  const ColEntries<Eng> ce(eng, a, reinterpret_cast<cx<double>*>(lds), c, true);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
     return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + pos]);
   };
-  if (a.colDesc) {
-    const ColDesc d = a.colDesc[c];
-    auto st = [&](int b, int pos, cx<T> v) {
-      const long long base = col_desc_base(d, a.colStride, pos);
-      if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
-    };
-#if SPFFT_ROW_STAGE
-    stage_rows(eng, lds, zl, n, load);
-    eng.lds_to_global(lds, tw, st);
-#else
-    eng.global_to_global(lds, tw, load, st);
-#endif
-    release_remote(a.remote);
-    return;
-  }
-  const int k0 = a.colOffsets[c];
-  const int ne = a.colOffsets[c + 1] - k0;
-  long long* cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
-  int* yEnt = reinterpret_cast<int*>(cBase + n);
-  for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
-  __syncthreads();
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    cBase[e] = a.colBase[k0 + e] + z0;
-    yEnt[a.colY[k0 + e]] = e;
-  }
-  __syncthreads();
   auto store = [&](int b, int pos, cx<T> v) {
-    const int e = yEnt[pos];
-    if (e >= 0 && b < zl) st_stream(&out[cBase[e] + b], cvt<typename BT::value_type>(v));
+    const long long base = ce.base(pos);
+    if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, zl, n, load);
