@@ -64,6 +64,65 @@ def _check_targets():
         gpus = [l for l in out.split() if "amdgcn" in l]
         if not gpus or any(not l.endswith("gfx950") for l in gpus):
             raise RuntimeError(f"{o}: unexpected offload targets {gpus}")
+    _check_kernel_resources(objs)
+
+
+# Stage kernels must not spill: a spill to scratch (private memory) in a stage
+# kernel costs far more than its HBM traffic. The gate fails the build when a
+# change makes a kernel spill. Round 2 found such a regression by profiling: a
+# second FFT call site put 188 B of scratch into the run-time-engine y stage.
+# The report lists VGPRs / scratch of every kernel in build/kernel_resources.txt.
+_SPILL_EXEMPT = ("fused",)  # opt-in persistent experiment (profiles/README.md)
+
+
+def _check_kernel_resources(objs):
+    llvm = os.path.join(ROCM, "llvm", "bin")
+    rows, bad = [], []
+    for o in sorted(objs):
+        fat, co = o + ".fatbin", o + ".gfx950.co"
+        try:
+            subprocess.run([os.path.join(llvm, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, o],
+                           check=True)
+            subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o",
+                            "--input=" + fat, "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                            "--output=" + co], check=True)
+            notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", co], check=True,
+                                   capture_output=True, text=True).stdout
+        finally:
+            for f in (fat, co):
+                if os.path.exists(f):
+                    os.remove(f)
+        name, meta = None, {}
+
+        def flush():
+            if name is None:
+                return
+            rows.append((name, meta.get("vgpr_count", "?"), meta.get("private_segment_fixed_size", "?"),
+                         meta.get("vgpr_spill_count", "?"), meta.get("sgpr_spill_count", "?")))
+            # a few bytes of stack (a small struct) are tolerated; register
+            # spills and real scratch traffic are not
+            spills = (int(meta.get("vgpr_spill_count", "0")) > 0 or
+                      int(meta.get("private_segment_fixed_size", "0")) > 64)
+            if spills and not any(x in name for x in _SPILL_EXEMPT):
+                bad.append(rows[-1])
+
+        for line in notes.splitlines():
+            t = line.strip()
+            if t.startswith(".name:"):
+                flush()
+                name, meta = t.split(":", 1)[1].strip(), {}
+            elif t.startswith((".vgpr_count:", ".private_segment_fixed_size:", ".vgpr_spill_count:",
+                               ".sgpr_spill_count:")):
+                k, v = t[1:].split(":", 1)
+                meta[k] = v.strip()
+        flush()
+    with open(os.path.join(BUILD_DIR, "kernel_resources.txt"), "w") as f:
+        f.write("kernel\tvgprs\tscratch_bytes_per_lane\tvgpr_spills\tsgpr_spills\n")
+        for r in rows:
+            f.write("\t".join(str(x) for x in r) + "\n")
+    if bad:
+        raise RuntimeError("stage kernels spill to scratch: " +
+                           "; ".join(f"{r[0][:80]} (vgprs {r[1]}, scratch {r[2]} B)" for r in bad[:5]))
 
 
 def main(argv=None):
