@@ -108,6 +108,16 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     // collective data-plane setup happens at plan time
     peerWrites_ = grid_->device_comm().peer_writes();
     if (peerWrites_) build_peer_tables();
+    localDirect_ = !peerWrites_ && env_int("SPFFT_LOCAL_DIRECT", 1, 0, 1) != 0;
+    if (localDirect_) {
+      // this rank's own block never moves: the z stage writes it straight into
+      // its place on the slab side (where the y stage and, forward, the z stage
+      // read it), so the exchange skips it instead of copying it on the device
+      std::vector<long long> sdl(sd);
+      sdl[p.rank] = slab_offset() + layout_.slabDispl[p.rank];
+      upload(segDispl_, sdl);
+      bwdSendCounts_[p.rank] = bwdRecvCounts_[p.rank] = 0;
+    }
     // exchange pipelining over plane chunks (build_chunk_plan). Automatic
     // choice: chunks only while the average per-peer message of a chunk stays
     // >= 4 MB (smaller RCCL messages lose link efficiency), at most 4; computed
@@ -243,6 +253,11 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
       c.rd.push_back(slabDispl[v] * eb);
       c.rc.push_back(static_cast<i64>(p.sticksPerRank[r]) * lk * eb);
     }
+    if (localDirect_) {
+      // own block in place on the slab side (see the constructor)
+      segDispl[k * P + me] = slab_offset() + slabDispl[k * P + me];
+      c.sc[me] = c.rc[me] = 0;
+    }
   }
   upload(zRank_, zSeg);
   upload(segDispl_, segDispl);
@@ -254,6 +269,18 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
   for (int k = 0; k < K; ++k) chunkEvents_.emplace_back(new GpuEvent());
   commDone_.reset(new GpuEvent());
   zDone_.reset(new GpuEvent());
+}
+
+// Element offset (exchange element type) from the stick-side buffer to the
+// slab-side buffer of this rank's grid.
+template <typename T>
+long long GpuExecutor<T>::slab_offset() const {
+  const i64 eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+  const char* stick = static_cast<const char*>(grid_->device_slot(GridImpl<T>::kStickSide));
+  const char* slab = static_cast<const char*>(grid_->device_slot(GridImpl<T>::kSlabSide));
+  const long long d = slab - stick;
+  if (d % eb != 0) throw InternalError();
+  return d / eb;
 }
 
 template <typename T>
@@ -865,7 +892,7 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
       ya.zBegin = xa.zBegin = planeBounds_[k];
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L <= ya.zBegin) continue;
-      ya.colBase = colBaseChunk_[k]->data<long long>();
+      ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
       set_col_desc(ya, colDescChunk_[k]);
       if (floatExchange_)
         dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
@@ -950,7 +977,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       ya.zBegin = xa.zBegin = planeBounds_[k];
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L > ya.zBegin) {
-        ya.colBase = colBaseChunk_[k]->data<long long>();
+        ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
         set_col_desc(ya, colDescChunk_[k]);
         dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
                                  twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
@@ -976,7 +1003,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     cx<T>* inter =
         interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (peerWrites_) {
-      ya.colBase = colBaseRemote_->data<long long>();
+      ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
       set_col_desc(ya, colDescRemote_);
       ya.remote = 1;
     }

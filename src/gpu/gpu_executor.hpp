@@ -122,6 +122,10 @@ private:
   // stage (forward) store straight into the receivers' buffers; these tables
   // hold those destinations as element offsets from the local buffer.
   bool peerWrites_ = false;
+  // RCCL / loopback data planes: this rank's own exchange block is written in
+  // place on the slab side instead of being copied (SPFFT_LOCAL_DIRECT=0 copies)
+  bool localDirect_ = false;
+  long long slab_offset() const;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
 
   // Fused single-GPU path (P = 1, C2C): plane-major sticks and the persistent

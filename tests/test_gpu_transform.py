@@ -538,3 +538,30 @@ def test_reference_size_sweep_full(gpu):
         if max(errs) > 1e-11:
             failures.append((dims, centered, errs))
     assert not failures, failures[:5]
+
+
+@pytest.mark.parametrize("exchange,chunks", [("COMPACT_BUFFERED", 3), ("UNBUFFERED", 1),
+                                             ("BUFFERED", 1)])
+def test_gpu_virtual_ranks_empty_transform(gpu, exchange, chunks, monkeypatch):
+    """No frequency values on any rank (a valid SpFFT transform): backward gives a zero
+    space domain, forward returns nothing, through every data plane and the chunk plan."""
+    import torch
+    from spfft_amd.parallel import run_ranks
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    dims = (16, 12, 10)
+    nx, ny, nz = dims
+    planes = [5, 5]
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        grid = sp.Grid(nx, ny, nz, 1, GPU, 1, max_local_z_length=5, comm=comm,
+                       exchange_type=getattr(sp.ExchangeType, exchange))
+        t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
+                                  np.zeros((0, 3), dtype=np.int32))
+        out = t.backward(torch.zeros(0, dtype=torch.complex128, device="cuda"))
+        zero = float(out.abs().max().item()) if out.numel() else 0.0
+        f = t.forward(None)
+        return zero, len(f)
+
+    for zero, nf in run_ranks(2, body):
+        assert zero == 0.0 and nf == 0
