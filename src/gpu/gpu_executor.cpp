@@ -48,8 +48,9 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
   chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
   // [z][column][y] (plane-major, default) or [column][z][y] intermediate
-  interColMajor_ = env_int("SPFFT_INTER_CMAJOR", 0, 0, 1) != 0;
-  interRing_ = chunkPlanes_ > 0 && !interColMajor_ && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
+  interLayout_ = env_int("SPFFT_INTER_LAYOUT", 0, 0, 2);
+  if (interLayout_ == 2 && p.num_columns() % 8 != 0) interLayout_ = 0;  // whole blocks only
+  interRing_ = chunkPlanes_ > 0 && interLayout_ == 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
   // launches in stream-ordered use (profiles/README.md, session 6)
@@ -714,14 +715,25 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
 }
 
 template <typename T>
-void GpuExecutor<T>::inter_strides(long long& zStride, long long& cStride) const {
+void GpuExecutor<T>::inter_strides(long long& zStride, long long& bStride, long long& cStride) const {
   const IndexPlan& p = *plan_;
-  if (interColMajor_) {
-    zStride = interStride_;
-    cStride = static_cast<long long>(p.local_planes()) * interStride_;
-  } else {
-    zStride = static_cast<long long>(p.num_columns()) * interStride_;
-    cStride = interStride_;
+  const long long S = interStride_;
+  const long long L = p.local_planes();
+  switch (interLayout_) {
+    case 1:  // column-major [c][z][y]
+      zStride = S;
+      cStride = L * S;
+      bStride = 8 * cStride;
+      break;
+    case 2:  // blocked [c/8][z][c%8][y]
+      zStride = 8 * S;
+      cStride = S;
+      bStride = 8 * L * S;
+      break;
+    default:  // plane-major [z][c][y]
+      zStride = static_cast<long long>(p.num_columns()) * S;
+      cStride = S;
+      bStride = 8 * S;
   }
 }
 
@@ -737,7 +749,7 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.n = p.dimY;
   a.colOfX0 = p.type == SPFFT_TRANS_R2C ? p.colOfX0 : -1;
   a.interStride = interStride_;
-  inter_strides(a.interZStride, a.interCStride);
+  inter_strides(a.interZStride, a.interBStride, a.interCStride);
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
@@ -756,7 +768,7 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   a.nFreq = p.dimXFreq;
   a.ncols = p.num_columns();
   a.interStride = interStride_;
-  inter_strides(a.interZStride, a.interCStride);
+  inter_strides(a.interZStride, a.interBStride, a.interCStride);
   a.colX = colX_ ? colX_->data<int>() : nullptr;
   return a;
 }

@@ -84,8 +84,10 @@ private:
   long long interStride_ = 0;  // row stride of [z][column][y]
   int chunkPlanes_ = 0;        // y/x stages interleaved per chunk of planes (0 = off)
   bool interRing_ = false;     // plane chunks share one chunk-sized intermediate (cache-resident)
-  bool interColMajor_ = false;  // SPFFT_INTER_CMAJOR=1: [column][z][y] intermediate
-  void inter_strides(long long& zStride, long long& cStride) const;
+  // SPFFT_INTER_LAYOUT: 0 plane-major [z][column][y] (default), 1 column-major
+  // [column][z][y], 2 blocked [column/8][z][column%8][y]
+  int interLayout_ = 0;
+  void inter_strides(long long& zStride, long long& bStride, long long& cStride) const;
   bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;
 

@@ -53,6 +53,10 @@ struct ColDesc {
   int len[kColRuns];  // 0 = unused run
 };
 
+__host__ __device__ inline long long inter_col(long long bStride, long long cStride, int c) {
+  return static_cast<long long>(c >> 3) * bStride + static_cast<long long>(c & 7) * cStride;
+}
+
 struct YArgs {
   int ncols;     // columns of the [z][column][y] intermediate (its row count per plane)
   int colBegin;  // column range processed: [colBegin, colEnd) (exchange pipelining chunks)
@@ -62,9 +66,12 @@ struct YArgs {
   int n;  // dimY
   int colOfX0;  // column needing the x=0 plane hermitian fill, -1 for none
   long long interStride;  // row stride of the [z][column][y] intermediate (>= n)
-  // row (z, column c) of the intermediate starts at z * interZStride + c * interCStride
-  // (plane-major: ncols*interStride, interStride; column-major: interStride, L*interStride)
-  long long interZStride, interCStride;
+  // row (z, column c) of the intermediate starts at
+  //   z * interZStride + (c / 8) * interBStride + (c % 8) * interCStride
+  // plane-major [z][c][y]:       ncols*S, 8*S,     S
+  // column-major [c][z][y]:      S,       8*L*S,   L*S
+  // blocked [c/8][z][c%8][y]:    8*S,     8*L*S,   S        (S = interStride)
+  long long interZStride, interBStride, interCStride;
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
@@ -82,7 +89,7 @@ struct XArgs {
   int nFreq;  // dimX/2+1 for R2C, dimX for C2C
   int ncols;
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
-  long long interZStride, interCStride;  // as YArgs
+  long long interZStride, interBStride, interCStride;  // as YArgs
   const int* colX;
 };
 

@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return eng.out_at(b, idx - b * n);
   }, [&](int idx, cx<T> v) {
     const int b = idx / n;
-    st_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + idx - b * n], v);
+    st_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + idx - b * n], v);
   });
 }
 
@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const ColEntries<Eng> ce(eng, a, reinterpret_cast<cx<double>*>(lds), c, true);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + c * a.interCStride + pos]);
+    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + pos]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const long long base = ce.base(pos);
@@ -976,10 +976,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xcol_of(a, xCol, n - pos);
-      return c < 0 ? czero<T>() : conj(ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]));
+      return c < 0 ? czero<T>() : conj(ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]));
     }
     const int c = xcol_of(a, xCol, pos);
-    return c < 0 ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
+    return c < 0 ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
@@ -1020,7 +1020,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const int c = xcol_of(a, xCol, pos);
-    if (c >= 0 && b < yl) st_inter(&dst[static_cast<long long>(c) * a.interCStride + b], v);
+    if (c >= 0 && b < yl) st_inter(&dst[inter_col(a.interBStride, a.interCStride, c) + b], v);
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
@@ -1064,7 +1064,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     // data, so its second read is served by the caches; plain loads keep it there)
     auto col = [&](int k, int b) -> cx<T> {
       const int c = xcol_of(a, xCol, k);
-      return (c < 0 || b >= yl) ? czero<T>() : src[static_cast<long long>(c) * a.interCStride + b];
+      return (c < 0 || b >= yl) ? czero<T>() : src[inter_col(a.interBStride, a.interCStride, c) + b];
     };
     eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
       cx<T> xk = col(k, b);
@@ -1089,14 +1089,14 @@ __global__ void __launch_bounds__(Eng::kBlock)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
     const int k = idx / B, b = idx - k * B;
     const int c = xcol_of(a, xCol, k);
-    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
+    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
   }, [&](int idx) {
     const int k = idx / B;
     return eng.in_at(idx - k * B, k);
   });
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int c = xcol_of(a, xCol, h);
-    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[static_cast<long long>(c) * a.interCStride + b]);
+    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
   }
   __syncthreads();
   // pre-pass in place, pairs (k, h-k): Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k
@@ -1160,7 +1160,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
     const cx<T> e = scale(yk + ym, T(0.5));
     const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
-    st_inter(&dst[static_cast<long long>(c) * a.interCStride + b], e + twm<-1>(o, twn[k]));
+    st_inter(&dst[inter_col(a.interBStride, a.interCStride, c) + b], e + twm<-1>(o, twn[k]));
   }
 }
 
