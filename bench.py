@@ -70,7 +70,7 @@ def _check(a, sp, t, values, gidx, dims, ttype, world):
     space = t.backward(values)
     torch.cuda.synchronize()
     err = {}
-    if world == 1:
+    if world == 1 and max(dims) <= 512:  # the dense numpy oracle (host memory, time)
         ref = dense_backward(gidx, values.cpu().numpy(), dims,
                              r2c=(ttype == sp.TransformType.R2C))
         err["backward_vs_numpy"] = max_rel_error(space.cpu().numpy(), ref)

@@ -211,6 +211,29 @@ struct CtShapeSel<double, 128, -1, false> : CtShape128E8 {};
 #ifndef SPFFT_WIDE_F256
 #define SPFFT_WIDE_F256 0
 #endif
+// measured at 1024^3 C2C fp64 (profiles/r2_s1/wide_ab.txt): 24.2 -> 47.0 transforms/s
+#ifndef SPFFT_WIDE_1024
+#define SPFFT_WIDE_1024 1
+#endif
+#if SPFFT_WIDE_1024
+// N = 1024 line-fast: with the 64 KB budget only 2 (fp64) / 8 (fp32) lines fit,
+// i.e. 32 / 64-byte column segments; these shapes take 8 / 16 lines (128-byte
+// segments) in one 139 KB workgroup of 512 threads per CU.
+struct CtShapeD1024W {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 4, kBudget = 150 * 1024, kMaxThr = 512;
+};
+struct CtShapeF1024W {
+  static constexpr int E = 32, R0 = 16, R1 = 16, R2 = 4, kBudget = 150 * 1024, kMaxThr = 512;
+};
+template <>
+struct CtShapeSel<double, 1024, 1, true> : CtShapeD1024W {};
+template <>
+struct CtShapeSel<double, 1024, -1, true> : CtShapeD1024W {};
+template <>
+struct CtShapeSel<float, 1024, 1, true> : CtShapeF1024W {};
+template <>
+struct CtShapeSel<float, 1024, -1, true> : CtShapeF1024W {};
+#endif
 #if SPFFT_WIDE_F512
 struct CtShapeF512W {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024, kMaxThr = 512;
