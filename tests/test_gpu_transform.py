@@ -565,3 +565,37 @@ def test_gpu_virtual_ranks_empty_transform(gpu, exchange, chunks, monkeypatch):
 
     for zero, nf in run_ranks(2, body):
         assert zero == 0.0 and nf == 0
+
+
+@pytest.mark.parametrize("dims", [(1024, 8, 12), (16, 1024, 8), (8, 12, 1024), (512, 16, 10),
+                                  (10, 512, 6)])
+@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("ttype", ["c2c", "r2c"])
+def test_long_lines(gpu, dims, single, ttype):
+    """Lengths 512 and 1024 along each axis: the wide (512-thread, up to 139 KB LDS)
+    line-fast shapes of the x/y stages and the row-mapped z shapes, fp64 and fp32."""
+    import torch
+    rng = np.random.default_rng(1024)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.6, 0.8, nx, ny, nz, r2c)[0]
+    G = sp.GridFloat if single else sp.Grid
+    grid = G(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    tol = 1e-4 if single else 1e-11
+    cdt = torch.complex64 if single else torch.complex128
+    if r2c:
+        space = rng.standard_normal((nz, ny, nx))
+        f = t.forward(torch.as_tensor(space.astype(np.float32 if single else np.float64), device=gpu))
+        assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < tol
+        b = t.backward(f)
+        ref = dense_backward(idx, f.cpu().numpy().astype(np.complex128), dims, r2c=True)
+        assert max_rel_error(b.cpu().numpy(), ref) < tol
+    else:
+        vals = _rand_vals(rng, len(idx), single)
+        out = t.backward(torch.as_tensor(vals, device=gpu, dtype=cdt))
+        assert max_rel_error(out.cpu().numpy(), dense_backward(idx, vals, dims)) < tol
+        space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+        f = t.forward(torch.as_tensor(space, device=gpu, dtype=cdt))
+        assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < tol
