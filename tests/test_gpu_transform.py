@@ -599,3 +599,44 @@ def test_long_lines(gpu, dims, single, ttype):
         space = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
         f = t.forward(torch.as_tensor(space, device=gpu, dtype=cdt))
         assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < tol
+
+
+@pytest.mark.parametrize("P,chunks", [(8, 1), (8, 2), (4, 3), (2, 4)])
+def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, monkeypatch):
+    """The driver's scaling configurations (2/4/8 ranks, the chunk counts the automatic
+    rule picks at 256^3) on virtual ranks of one GPU, with a sphere split evenly like
+    bench.py: multi_transform of 2 transforms per rank, backward vs numpy, round trip."""
+    import torch
+    from spfft_amd.parallel import TorchDistComm, make_distributed, run_ranks  # noqa: F401
+    from spfft_amd.utils.indices import distribute_sticks
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    dims = (48, 40, 64)
+    nx, ny, nz = dims
+    gidx = sphere_indices(*dims, 0.5)
+    parts = distribute_sticks(gidx, P, dims)
+    planes = [nz // P + (1 if r < nz % P else 0) for r in range(P)]
+    offsets = np.concatenate([[0], np.cumsum(planes)])
+    rng = np.random.default_rng(88)
+    vals = [_rand_vals(rng, len(gidx)) for _ in range(2)]
+    refs = [dense_backward(gidx, v, dims) for v in vals]
+    starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
+    max_sticks = max(len(np.unique(p[:, 0] * ny + p[:, 1])) for p in parts)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        ts = []
+        for _ in range(2):
+            g = sp.Grid(nx, ny, nz, max_sticks, GPU, 1, max_local_z_length=max(planes), comm=comm,
+                        exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+            ts.append(g.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
+                                         parts[rank]))
+        ins = [torch.as_tensor(v[starts[rank]:starts[rank + 1]], device="cuda") for v in vals]
+        outs = sp.multi_transform_backward(ts, ins)
+        e = max(max_rel_error(o.cpu().numpy(), r[offsets[rank]:offsets[rank + 1]])
+                for o, r in zip(outs, refs))
+        back = sp.multi_transform_forward(ts, scalings=[sp.Scaling.FULL] * 2)
+        e2 = max(max_rel_error(b.cpu().numpy(), i.cpu().numpy()) for b, i in zip(back, ins))
+        return max(e, e2)
+
+    for e in run_ranks(P, body):
+        assert e < 1e-11
