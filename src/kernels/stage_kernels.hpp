@@ -805,7 +805,7 @@ struct ColEntries {
   int* yEnt;         // LDS: y -> entry or -1 (list mode)
   int* cY;           // LDS: entry -> y (list mode)
   int ne;
-  __device__ ColEntries(const Eng& eng, const YArgs& a, cx<double>* ldsBase, int c, bool allowDesc) {
+  __device__ ColEntries(const Eng& eng, const YArgs& a, void* ldsBase, int c, bool allowDesc) {
     const int n = eng.n();
     useDesc = allowDesc && a.colDesc != nullptr;
     stride = a.colStride;
@@ -852,7 +852,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   const bool x0 = c == a.colOfX0;
-  const ColEntries<Eng> ce(eng, a, reinterpret_cast<cx<double>*>(lds), c, !x0);
+  const ColEntries<Eng> ce(eng, a, lds, c, !x0);
   auto load = [&](int b, int pos) -> cx<T> {
     const long long base = ce.base(pos);
     if (base == kNoColEntry || b >= zl) return czero<T>();
@@ -910,7 +910,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
-  const ColEntries<Eng> ce(eng, a, reinterpret_cast<cx<double>*>(lds), c, true);
+  const ColEntries<Eng> ce(eng, a, lds, c, true);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
     return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + pos]);
