@@ -38,7 +38,7 @@ private:
   const std::function<void(std::int64_t, std::int64_t, int)>* job_ = nullptr;
   std::int64_t jobN_ = 0, jobGrain_ = 1;
   std::atomic<std::int64_t> next_{0};
-  std::uint64_t generation_ = 0;
+  std::atomic<std::uint64_t> generation_{0};
   int running_ = 0;
   bool stop_ = false;
   std::exception_ptr error_;
