@@ -199,6 +199,67 @@ struct CtEng {
   static std::size_t h_lds() { return F::lds_bytes(); }
 };
 
+// Paired fp32 line-fast engine: the FFT core runs on cx<f2> (lines 2p and 2p+1
+// in one lane, packed fp32 arithmetic) while the stage kernels keep addressing
+// single complex<float> lines: lane pair p carries lines p and p + F::B, so each
+// load/store instruction of a wave covers the same contiguous line run as the
+// unpaired engine; the LDS tile keeps each pair as two adjacent complex<float>
+// values (lds_put/lds_get).
+#ifndef SPFFT_F32_PAIR
+#define SPFFT_F32_PAIR 0  // measured slower: profiles/r2_s1/pair_ab.txt
+#endif
+template <int N, int S>
+struct CtEngPair {
+  using F = FftCT<f2, N, S, true>;
+  static constexpr bool kBatchedCopy = false;
+  static constexpr bool kLineFast = true;
+  static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
+  __device__ int lines() const { return 2 * F::B; }
+  __device__ int n() const { return N; }
+  __device__ int in_at(int b, int pos) const { return 2 * F::in_at(b % F::B, pos) + b / F::B; }
+  __device__ int out_at(int b, int pos) const { return 2 * F::out_at(b % F::B, pos) + b / F::B; }
+  __device__ int input_elems() const { return 2 * F::B * F::LS; }
+  __device__ int lds_bytes() const { return static_cast<int>(F::lds_bytes()); }
+  static __device__ cx<f2>* pairs(cx<float>* lds) { return reinterpret_cast<cx<f2>*>(lds); }
+  template <class Ld>
+  static __device__ auto pair_load(Ld& ld) {
+    return [&](int p, int pos) -> cx<f2> {
+      const cx<float> a = ld(p, pos), b = ld(p + F::B, pos);
+      f2 re, im;
+      re.x = a.x;
+      re.y = b.x;
+      im.x = a.y;
+      im.y = b.y;
+      return mk<f2>(re, im);
+    };
+  }
+  template <class St>
+  static __device__ auto pair_store(St& st) {
+    return [&](int p, int pos, cx<f2> v) {
+      st(p, pos, mk<float>(v.x.x, v.y.x));
+      st(p + F::B, pos, mk<float>(v.x.y, v.y.y));
+    };
+  }
+  template <class St>
+  __device__ void lds_to_global(cx<float>* lds, const cx<float>* __restrict__ tw, St st) const {
+    F::run(pairs(lds), tw, NoLoad{}, pair_store(st));
+  }
+  template <class Ld>
+  __device__ void global_to_lds(cx<float>* lds, const cx<float>* __restrict__ tw, Ld ld) const {
+    F::run_to_lds(pairs(lds), tw, pair_load(ld));
+  }
+  __device__ void lds_to_lds(cx<float>* lds, const cx<float>* __restrict__ tw) const {
+    F::run_to_lds(pairs(lds), tw, NoLoad{});
+  }
+  template <class Ld, class St>
+  __device__ void global_to_global(cx<float>* lds, const cx<float>* __restrict__ tw, Ld ld, St st) const {
+    F::run(pairs(lds), tw, pair_load(ld), pair_store(st));
+  }
+  static int h_lines() { return 2 * F::B; }
+  static int h_threads() { return F::NT; }
+  static std::size_t h_lds() { return F::lds_bytes(); }
+};
+
 // Run-time length engine. LF (line-fast) engines walk the global side with the
 // line index fastest — consecutive lanes touch consecutive lines, i.e. the
 // contiguous z-run of a stick or y-run of an intermediate column — like the
@@ -1195,8 +1256,13 @@ inline void with_engine(int n, F&& f) {
   switch (n) {
 #define SPFFT_CT_CASE(NN)                                                         \
   case NN: {                                                                      \
-    using E = CtEng<T, NN, S, LF>;                                                \
-    f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                             \
+    if constexpr (SPFFT_F32_PAIR && LF && std::is_same<T, float>::value && NN >= 64) { \
+      using E = CtEngPair<NN, S>;                                                 \
+      f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                           \
+    } else {                                                                      \
+      using E = CtEng<T, NN, S, LF>;                                              \
+      f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                           \
+    }                                                                             \
     return;                                                                       \
   }
     SPFFT_CT_CASE(16)
