@@ -631,6 +631,20 @@ __device__ __forceinline__ int block_tile_x() {
   return bx;
 }
 
+// Reversed tile order for a stage that reads what the previous stage wrote
+// (SPFFT_REVERSE_READS bit mask): the most recently written data, the part
+// still held in the 256 MB memory-side Infinity Cache, is read first.
+//   1: y backward columns (z backward wrote the sticks column by column)
+//   2: x forward planes (x backward wrote the space planes in order)
+//   4: z forward sticks (y forward wrote the sticks column by column)
+#ifndef SPFFT_REVERSE_READS
+#define SPFFT_REVERSE_READS 0  // within noise: profiles/r2_s1/reverse_reads.txt
+#endif
+template <int Bit>
+__device__ __forceinline__ int tile_order(int t, int n) {
+  return (SPFFT_REVERSE_READS & Bit) ? n - 1 - t : t;
+}
+
 // ---------------------------------------------------------------- z stage
 template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
@@ -689,7 +703,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
                      T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const int s0 = a.stickBegin + block_tile_x() * B;
+  const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
@@ -781,7 +795,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
                           T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const int s0 = a.stickBegin + block_tile_x() * B;
+  const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
   const int nl = min(B, a.numSticks - s0);
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
@@ -909,7 +923,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = a.colBegin + y_tile_col();
+  const int c = a.colBegin + tile_order<1>(y_tile_col(), SPFFT_Y_ZFAST ? gridDim.y : gridDim.x);
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   const bool x0 = c == a.colOfX0;
@@ -1067,7 +1081,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   int tx, ty;
   block_tile(tx, ty);
-  const int zl = a.zBegin + ty;
+  const int zl = a.zBegin + tile_order<2>(ty, gridDim.y);
   const int y0 = tx * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, n);
@@ -1194,7 +1208,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const long long n = 2 * static_cast<long long>(h);
   int tx, ty;
   block_tile(tx, ty);
-  const int zl = a.zBegin + ty;
+  const int zl = a.zBegin + tile_order<2>(ty, gridDim.y);
   const int y0 = tx * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, h + 1);
