@@ -514,6 +514,234 @@ struct FftCT {
   }
 };
 
+// ------------------------------------------------ compile-time mixed radix
+// Lengths built from the codelet radices that are not powers of two (240 =
+// 16 * 15, 200 = 20 * 10, 192 = 16 * 12, ...) get the FftCT treatment instead
+// of the run-time engine: the first pass is loaded straight from global memory,
+// the last pass stored straight from registers, the passes in between
+// exchanged through LDS, and every index is a compile-time constant. A pass of
+// radix R has N / R butterflies, spread over the line's TP lanes (lanes past
+// the count idle in that pass). mr_plan picks the radices (at most 4 passes,
+// non-increasing) and TP that minimise the padded lane work sum_i TP * ceil(N /
+// R_i / TP) * R_i under a register cap per lane (mr_sel).
+// Plan limits per stage kind, measured on MI355X at 192^3, 200^3 and 240^3
+// (profiles/r2_s1/mr_ab.txt): the forward stages run fastest with the
+// fewest passes (up to 20 elements per lane, 200 = 20 * 10); the backward
+// stages with at most 16 (200 = 10 * 10 * 2); the fp64 backward line-fast
+// stages (the y stage's sparse stick loads) with at least 32 lanes per line;
+// the row-mapped z stages with 256-thread workgroups.
+struct MrSel {
+  int emax, minTp, maxThr;
+};
+template <typename T, int S, bool LF>
+__host__ __device__ constexpr MrSel mr_sel() {
+  if (S < 0) return MrSel{20, 2, 256};
+  if (!LF) return MrSel{16, 2, 256};
+  return MrSel{16, sizeof(T) == 8 ? 32 : 2, 512};
+}
+
+struct MrPlan {
+  int np, r[4], tp, e, cost;
+};
+
+__host__ __device__ constexpr bool mr_codelet(int r) {
+  return (r >= 2 && r <= 13) || r == 15 || r == 16 || r == 20;
+}
+__host__ __device__ constexpr int mr_cdiv(int a, int b) { return (a + b - 1) / b; }
+
+__host__ __device__ constexpr MrPlan mr_score(int n, MrPlan p, int emax, int minTp) {
+  p.tp = 0;
+  p.cost = 1 << 30;
+  for (int tp = minTp; tp <= 64; ++tp) {
+    int cost = 0, e = 0;
+    for (int i = 0; i < p.np; ++i) {
+      const int k = mr_cdiv(n / p.r[i], tp);
+      cost += tp * k * p.r[i];
+      if (k * p.r[i] > e) e = k * p.r[i];
+    }
+    if (e > emax) continue;
+    if (cost < p.cost || (cost == p.cost && e < p.e)) {
+      p.tp = tp;
+      p.e = e;
+      p.cost = cost;
+    }
+  }
+  return p;
+}
+
+__host__ __device__ constexpr void mr_search(int n, int m, MrPlan cur, int maxr, int emax,
+                                             int minTp, MrPlan& best) {
+  if (m == 1) {
+    const MrPlan s = mr_score(n, cur, emax, minTp);
+    if (s.tp && s.cost < best.cost) best = s;
+    return;
+  }
+  if (cur.np == 4) return;
+  for (int a = maxr; a >= 2; --a) {
+    if (!mr_codelet(a) || m % a) continue;
+    MrPlan next = cur;
+    next.r[next.np++] = a;
+    mr_search(n, m / a, next, a, emax, minTp, best);
+  }
+}
+
+__host__ __device__ constexpr MrPlan mr_plan(int n, int emax, int minTp) {
+  MrPlan best{0, {1, 1, 1, 1}, 0, 0, 1 << 30};
+  mr_search(n, n, MrPlan{0, {1, 1, 1, 1}, 0, 0, 0}, 20, emax, minTp, best);
+  return best;
+}
+
+// Same interface and lane mapping as FftCT (LF: lines fastest).
+template <typename T, int N, int S, bool LF = false>
+struct FftMR {
+  static constexpr MrSel Sel = mr_sel<T, S, LF>();
+  static constexpr MrPlan P = mr_plan(N, Sel.emax, Sel.minTp);
+  static_assert(P.np > 0, "length has no mixed-radix plan");
+  static constexpr int NP = P.np;
+  static constexpr int TP = P.tp;
+  static constexpr int E = P.e;
+  static constexpr int LS0 = padded_stride<T>(N);
+  static constexpr int kMaxThr = Sel.maxThr;
+  static constexpr int B0 =
+      lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), kLdsBudget, kMaxThr);
+  static constexpr int B = LF ? lf_lines(B0) : B0;
+  static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B) : LS0;
+  static constexpr int NT = B * TP;
+
+  static constexpr int lines() { return B; }
+  static constexpr int threads() { return NT; }
+  static constexpr std::size_t lds_bytes() { return std::size_t(B) * LS * sizeof(cx<T>); }
+  __device__ static int in_at(int b, int pos) { return b * LS + pad_index<T>(pos); }
+  __device__ static int out_at(int b, int pos) { return b * LS + pad_index<T>(pos); }
+  __device__ static int lane_line() { return LF ? threadIdx.x % B : threadIdx.x / TP; }
+  __device__ static int lane_pos() { return LF ? threadIdx.x / B : threadIdx.x % TP; }
+
+  template <int I>
+  static constexpr int radix() { return P.r[I]; }
+  template <int I>
+  static constexpr int stride_ns() {  // product of the radices before pass I
+    int ns = 1;
+    for (int i = 0; i < I; ++i) ns *= P.r[i];
+    return ns;
+  }
+  template <int I>
+  static constexpr int iters() { return mr_cdiv(N / radix<I>(), TP); }
+  template <int I>
+  __device__ static bool active(int j) { return (N / radix<I>()) % TP == 0 || j < N / radix<I>(); }
+
+  // pass I inputs: v[k*R + r] = element j + r*N/R of the line, j = t + k*TP
+  template <int I, class Load>
+  __device__ static void gather(cx<T> (&v)[E], const cx<T>* line, Load load, int b, int t) {
+    constexpr int R = radix<I>(), NB = N / R;
+#pragma unroll
+    for (int k = 0; k < iters<I>(); ++k) {
+      const int j = t + k * TP;
+      if (!active<I>(j)) continue;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (std::is_same<Load, NoLoad>::value)
+          v[k * R + r] = lds_get(&line[pad_index<T>(j + r * NB)]);
+        else
+          v[k * R + r] = load(b, j + r * NB);
+      }
+    }
+  }
+
+  template <int I>
+  __device__ static void butterflies(cx<T> (&v)[E], int t, const cx<T>* __restrict__ tw) {
+    constexpr int R = radix<I>(), NS = stride_ns<I>();
+#pragma unroll
+    for (int k = 0; k < iters<I>(); ++k) {
+      const int j = t + k * TP;
+      if (!active<I>(j)) continue;
+      if (NS > 1) {
+        const int kk = j % NS;
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+          v[k * R + r] = twm<S>(v[k * R + r], tw[kk * r * (N / (NS * R))]);
+      }
+      Dft<R, S, T>::run(&v[k * R]);
+    }
+  }
+
+  // pass I outputs to their Stockham positions in LDS
+  template <int I>
+  __device__ static void scatter(cx<T> (&v)[E], cx<T>* line, int t) {
+    constexpr int R = radix<I>(), NS = stride_ns<I>();
+#pragma unroll
+    for (int k = 0; k < iters<I>(); ++k) {
+      const int j = t + k * TP;
+      if (!active<I>(j)) continue;
+      const int kk = j % NS;
+      const int base = (j - kk) * R + kk;
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds_put(&line[pad_index<T>(base + r * NS)], v[k * R + r]);
+    }
+  }
+
+  template <int I>
+  __device__ static void later_passes(cx<T> (&v)[E], cx<T>* line, int t, const cx<T>* __restrict__ tw) {
+    __syncthreads();
+    scatter<I - 1>(v, line, t);
+    __syncthreads();
+    gather<I>(v, line, NoLoad{}, 0, t);
+    butterflies<I>(v, t, tw);
+    if constexpr (I + 1 < NP) later_passes<I + 1>(v, line, t, tw);
+  }
+
+  template <class Load>
+  __device__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<T>* __restrict__ tw,
+                                   Load load, int b, int t) {
+    cx<T>* line = lds + b * LS;
+    gather<0>(v, line, load, b, t);
+    butterflies<0>(v, t, tw);
+    if constexpr (NP > 1) later_passes<1>(v, line, t, tw);
+  }
+
+  // Result delivered to store(b, pos, value), only for the lane's own line
+  // (the FftCT contract); consecutive lanes -> consecutive positions.
+  template <class Load, class Store>
+  __device__ static void run(cx<T>* lds, const cx<T>* __restrict__ tw, Load load, Store store) {
+    const int b = lane_line(), t = lane_pos();
+    cx<T> v[E];
+    transform(v, lds, tw, load, b, t);
+    constexpr int RL = radix<NP - 1>(), NB = N / RL;
+#pragma unroll
+    for (int k = 0; k < iters<NP - 1>(); ++k) {
+      const int j = t + k * TP;
+      if (!active<NP - 1>(j)) continue;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) store(b, j + r * NB, v[k * RL + r]);
+    }
+  }
+
+  // Result left in LDS at out_at(b, pos); ends with a barrier.
+  template <class Load>
+  __device__ static void run_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Load load) {
+    const int b = lane_line(), t = lane_pos();
+    cx<T> v[E];
+    transform(v, lds, tw, load, b, t);
+    __syncthreads();
+    cx<T>* line = lds + b * LS;
+    constexpr int RL = radix<NP - 1>(), NB = N / RL;
+#pragma unroll
+    for (int k = 0; k < iters<NP - 1>(); ++k) {
+      const int j = t + k * TP;
+      if (!active<NP - 1>(j)) continue;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) lds_put(&line[pad_index<T>(j + r * NB)], v[k * RL + r]);
+    }
+    __syncthreads();
+  }
+};
+
+// Compile-time engine core of a length: FftCT for powers of two, else FftMR.
+template <typename T, int N, int S, bool LF>
+struct CtCore {
+  using type = typename std::conditional<(N & (N - 1)) == 0, FftCT<T, N, S, LF>,
+                                         FftMR<T, N, S, LF>>::type;
+};
+
 // ---------------------------------------------------------------- RT engine
 struct RtPlan {
   int n;       // length

@@ -121,8 +121,23 @@ void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
 
 // Largest run-time FFT length supported in one workgroup (LDS-resident).
 int max_device_fft_length(bool doublePrecision);
-// true if n has a compile-time (register-resident) kernel.
+// true if n has a compile-time (register-resident) kernel: the powers of two
+// 16..1024 (FftCT) and the mixed-radix lengths of SPFFT_MR_SIZES (FftMR).
 bool has_ct_kernel(int n);
+
+// Non-power-of-two lengths with compile-time mixed-radix kernels (X-macro).
+#ifndef SPFFT_MR
+#define SPFFT_MR 1
+#endif
+#ifndef SPFFT_MR_SIZES
+#if SPFFT_MR
+#define SPFFT_MR_SIZES(X)                                                                 \
+  X(96) X(120) X(144) X(160) X(180) X(192) X(200) X(216) X(240) X(288) X(320) X(360) X(384) \
+  X(400) X(480)
+#else
+#define SPFFT_MR_SIZES(X)
+#endif
+#endif
 
 }  // namespace dev
 }  // namespace spfft

@@ -168,7 +168,7 @@ __device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, S
 // ------------------------------------------------------------ engine adapters
 template <typename T, int N, int S, bool LF = false>
 struct CtEng {
-  using F = FftCT<T, N, S, LF>;
+  using F = typename CtCore<T, N, S, LF>::type;
   static constexpr bool kBatchedCopy = false;
   static constexpr bool kLineFast = LF;
   static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
@@ -1270,7 +1270,8 @@ inline void with_engine(int n, F&& f) {
   switch (n) {
 #define SPFFT_CT_CASE(NN)                                                         \
   case NN: {                                                                      \
-    if constexpr (SPFFT_F32_PAIR && LF && std::is_same<T, float>::value && NN >= 64) { \
+    if constexpr (SPFFT_F32_PAIR && LF && std::is_same<T, float>::value &&          \
+                  NN >= 64 && (NN & (NN - 1)) == 0) {                             \
       using E = CtEngPair<NN, S>;                                                 \
       f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                           \
     } else {                                                                      \
@@ -1286,6 +1287,9 @@ inline void with_engine(int n, F&& f) {
     SPFFT_CT_CASE(256)
     SPFFT_CT_CASE(512)
     SPFFT_CT_CASE(1024)
+#define SPFFT_MR_CASE(NN) SPFFT_CT_CASE(NN)
+    SPFFT_MR_SIZES(SPFFT_MR_CASE)
+#undef SPFFT_MR_CASE
 #undef SPFFT_CT_CASE
     default: {
       if (use_bluestein(n, sizeof(cx<T>))) {

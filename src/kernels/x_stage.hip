@@ -260,7 +260,15 @@ BlueTables bluestein_tables(int n, bool dbl) {
 int max_device_fft_length(bool dbl) { return (160 * 1024) / (2 * (dbl ? 16 : 8)) - 1; }
 
 bool has_ct_kernel(int n) {
-  return n == 16 || n == 32 || n == 64 || n == 128 || n == 256 || n == 512 || n == 1024;
+  switch (n) {
+    case 16: case 32: case 64: case 128: case 256: case 512: case 1024:
+#define SPFFT_MR_HAS(NN) case NN:
+    SPFFT_MR_SIZES(SPFFT_MR_HAS)
+#undef SPFFT_MR_HAS
+      return true;
+    default:
+      return false;
+  }
 }
 
 }  // namespace dev

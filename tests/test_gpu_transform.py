@@ -194,6 +194,40 @@ def test_composite_radices(gpu, dims, ttype, single):
     assert max_rel_error(f.cpu().numpy(), dense_forward(space.astype(np.complex128), idx, dims)) < tol
 
 
+@pytest.mark.parametrize("dims", [(240, 12, 10), (10, 200, 12), (12, 10, 192), (192, 240, 200),
+                                  (96, 144, 216), (360, 8, 10), (6, 480, 8), (10, 6, 384)])
+@pytest.mark.parametrize("ttype", ["c2c", "r2c"])
+@pytest.mark.parametrize("single", [False, True])
+def test_mixed_radix_ct_lengths(gpu, dims, ttype, single):
+    """The compile-time mixed-radix kernels (FftMR, SPFFT_MR_SIZES: 2- and 3-pass
+    plans such as 240 = 16*15, 200 = 20*10 / 10*10*2, 216 = 12*6*3) on every axis:
+    z row engine, y/x line-fast engines, packed-real x stage on N/2."""
+    import torch
+    rng = np.random.default_rng(29)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.8, 0.8, nx, ny, nz, r2c)[0]
+    if r2c:
+        vals = dense_forward(rng.standard_normal((nz, ny, nx)), idx, dims)
+    else:
+        vals = _rand_vals(rng, len(idx))
+    vals = vals.astype(np.complex64 if single else np.complex128)
+    grid = (sp.GridFloat if single else sp.Grid)(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    out = t.backward(torch.as_tensor(vals, device=gpu))
+    ref = dense_backward(idx, vals.astype(np.complex128), dims, r2c=r2c)
+    tol = 2e-5 if single else 1e-12
+    assert max_rel_error(out.cpu().numpy(), ref) < tol
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    space = space.astype((np.float32 if r2c else np.complex64) if single else
+                         (np.float64 if r2c else np.complex128))
+    f = t.forward(torch.as_tensor(space, device=gpu))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space.astype(np.complex128), idx, dims)) < tol
+
+
 def test_host_pointers_on_gpu_transform(gpu):
     """GPU transform with host input/output and host space domain (staging paths)."""
     rng = np.random.default_rng(4)
