@@ -18,32 +18,12 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
   });
 }
 
-template <typename T, typename BT>
-void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* tw,
-                      hipStream_t stream) {
-  if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
-  with_engine<T, -1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
-    auto k = y_forward_kernel<decltype(eng), T, BT>;
-    const std::size_t ldsTotal = lds + std::size_t(a.n) * (sizeof(long long) + sizeof(int)) + 16;
-    prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
-                       inter, out, tw);
-    gpu_check_launch("y_forward", stream);
-  });
-}
-
 template void launch_y_backward<double, cx<double>>(const YArgs&, const cx<double>*, cx<double>*,
                                                     const cx<double>*, hipStream_t);
 template void launch_y_backward<double, cx<float>>(const YArgs&, const cx<float>*, cx<double>*,
                                                    const cx<double>*, hipStream_t);
 template void launch_y_backward<float, cx<float>>(const YArgs&, const cx<float>*, cx<float>*,
                                                   const cx<float>*, hipStream_t);
-template void launch_y_forward<double, cx<double>>(const YArgs&, const cx<double>*, cx<double>*,
-                                                   const cx<double>*, hipStream_t);
-template void launch_y_forward<double, cx<float>>(const YArgs&, const cx<double>*, cx<float>*,
-                                                  const cx<double>*, hipStream_t);
-template void launch_y_forward<float, cx<float>>(const YArgs&, const cx<float>*, cx<float>*,
-                                                 const cx<float>*, hipStream_t);
 
 }  // namespace dev
 }  // namespace spfft

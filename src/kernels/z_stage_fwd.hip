@@ -1,0 +1,31 @@
+// z-stage forward launcher: unpack / z-FFT / compress with scaling (its own
+// translation unit so the z-stage kernels compile in parallel).
+#include "kernels/stage_kernels.hpp"
+
+namespace spfft {
+namespace dev {
+
+template <typename T, typename BT>
+void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, const cx<T>* tw,
+                      hipStream_t stream) {
+  if (a.numSticks <= a.stickBegin) return;
+  with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
+    auto k = a.desc ? z_forward_desc_kernel<decltype(eng), T, BT>
+                    : z_forward_kernel<decltype(eng), T, BT>;
+    const std::size_t ldsTotal = lds + run_table_bytes(lines);
+    prepare_kernel(k, ldsTotal);
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+                       in, values, scale, tw);
+    gpu_check_launch("z_forward", stream);
+  });
+}
+
+template void launch_z_forward<double, cx<double>>(const ZArgs&, const cx<double>*, cx<double>*,
+                                                   double, const cx<double>*, hipStream_t);
+template void launch_z_forward<double, cx<float>>(const ZArgs&, const cx<float>*, cx<double>*,
+                                                  double, const cx<double>*, hipStream_t);
+template void launch_z_forward<float, cx<float>>(const ZArgs&, const cx<float>*, cx<float>*, float,
+                                                 const cx<float>*, hipStream_t);
+
+}  // namespace dev
+}  // namespace spfft
