@@ -167,27 +167,32 @@ void GpuExecutor<T>::build_col_desc(ColDescTable& t, const std::vector<long long
   t.buf.reset();
   t.stride = stride;
   if (!colDescs_ || p.num_columns() < 1) return;
+  // the kernels form y * stride in 32 bits
+  if (static_cast<long long>(p.dimY) * stride >= (1LL << 31)) return;
   std::vector<dev::ColDesc> d(p.num_columns());
   for (int c = 0; c < p.num_columns(); ++c) {
     dev::ColDesc& q = d[c];
+    std::vector<long long> first(dev::kColRuns, 0);
     for (int r = 0; r < dev::kColRuns; ++r) {
-      q.base[r] = 0;
+      q.b0[r] = 0;
       q.y[r] = 0;
       q.len[r] = 0;
     }
     int r = -1;
     for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e) {
       const bool extend = r >= 0 && p.colY[e] == q.y[r] + q.len[r] &&
-                          colBase[e] == q.base[r] + static_cast<long long>(q.len[r]) * stride;
+                          colBase[e] == first[r] + static_cast<long long>(q.len[r]) * stride;
       if (extend) {
         ++q.len[r];
         continue;
       }
       if (++r >= dev::kColRuns) return;  // too fragmented: LDS-staged entry lists
-      q.base[r] = colBase[e];
+      first[r] = colBase[e];
       q.y[r] = p.colY[e];
       q.len[r] = 1;
     }
+    q.nRuns = r + 1;
+    for (int k = 0; k < q.nRuns; ++k) q.b0[k] = first[k] - static_cast<long long>(q.y[k]) * stride;
   }
   upload(t.buf, d);
 }

@@ -38,19 +38,18 @@ struct ZArgs {
   int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
 };
 
-// "no stick at this y" marker of a column lookup (bases of the peer-write
-// tables are offsets to other GPUs' buffers and may be negative)
-constexpr long long kNoColEntry = -(1LL << 62);
 
 // A column's stick entries as at most kColRuns runs with consecutive y and
-// consecutive bases (base of y = base[r] + (y - y[r]) * YArgs::colStride). A
-// sphere column is two runs (storage y = 0..h and n-h..n-1); entries from
-// several ranks add runs. Workgroup-uniform, so it lives in scalar registers.
+// consecutive bases: y in run r (y - y[r] < len[r]) has its entry at b0[r] +
+// y * YArgs::colStride (b0 = the run's first base - y[r] * colStride). A sphere
+// column is two runs (storage y = 0..h and n-h..n-1); entries from several
+// ranks add runs. Workgroup-uniform, so it lives in scalar registers.
 constexpr int kColRuns = 4;
 struct ColDesc {
-  long long base[kColRuns];
+  long long b0[kColRuns];
   int y[kColRuns];
-  int len[kColRuns];  // 0 = unused run
+  int len[kColRuns];
+  int nRuns;
 };
 
 __host__ __device__ inline long long inter_col(long long bStride, long long cStride, int c) {

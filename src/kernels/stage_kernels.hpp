@@ -854,15 +854,22 @@ inline dim3 y_grid(int cols, int zblocks) {
 }
 
 // ---------------------------------------------------------------- y stage
-// Base of the stick entry at y of a column with a run descriptor, or kNoColEntry.
-__device__ __forceinline__ long long col_desc_base(const ColDesc& d, long long stride, int y) {
-  long long base = kNoColEntry;
+// Whether the column with run descriptor d has a stick entry at y, and its base
+// (uniform loop bound nRuns: a sphere column tests its 2 runs only).
+__device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride, int y,
+                                              long long& base) {
+  long long b0 = 0;
+  bool hit = false;
 #pragma unroll
   for (int r = 0; r < kColRuns; ++r) {
-    const unsigned off = static_cast<unsigned>(y - d.y[r]);
-    if (off < static_cast<unsigned>(d.len[r])) base = d.base[r] + static_cast<long long>(off) * stride;
+    if (r < d.nRuns) {
+      const bool in = static_cast<unsigned>(y - d.y[r]) < static_cast<unsigned>(d.len[r]);
+      b0 = in ? d.b0[r] : b0;
+      hit = hit || in;
+    }
   }
-  return base;
+  base = b0 + static_cast<long long>(static_cast<unsigned>(y) * static_cast<unsigned>(stride));
+  return hit;
 }
 
 // Stick entries of the workgroup's column: through the column's run descriptor
@@ -904,11 +911,12 @@ struct ColEntries {
     }
     __syncthreads();
   }
-  // base of the entry at y (add the plane), or kNoColEntry
-  __device__ long long base(int y) const {
-    if (useDesc) return col_desc_base(d, stride, y);
+  // whether the column has an entry at y; its base (add the plane) in base
+  __device__ bool find(int y, long long& base) const {
+    if (useDesc) return col_desc_find(d, stride, y, base);
     const int e = yEnt[y];
-    return e < 0 ? kNoColEntry : cBase[e];
+    base = e < 0 ? 0 : cBase[e];
+    return e >= 0;
   }
 };
 
@@ -929,8 +937,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const bool x0 = c == a.colOfX0;
   const ColEntries<Eng> ce(eng, a, lds, c, !x0);
   auto load = [&](int b, int pos) -> cx<T> {
-    const long long base = ce.base(pos);
-    if (base == kNoColEntry || b >= zl) return czero<T>();
+    long long base;
+    if (!ce.find(pos, base) || b >= zl) return czero<T>();
     return cvt<T>(ld_stream(&in[base + z0 + b]));
   };
   // the x = 0 column of an R2C transform: gathered into LDS, hermitian fill
@@ -991,8 +999,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + pos]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
-    const long long base = ce.base(pos);
-    if (base != kNoColEntry && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+    long long base;
+    if (ce.find(pos, base) && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, zl, n, load);
