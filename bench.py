@@ -50,6 +50,10 @@ def parse():
                     help="independent transforms per step, run with multi_transform_backward/"
                          "forward on one stream each (the reference benchmark's -m): one "
                          "transform's all-to-all overlaps the others' FFT kernels")
+    ap.add_argument("--streams", default="per-transform", choices=["per-transform", "one"],
+                    help="with --sync stream and T > 1: one stream per transform (their kernels "
+                         "overlap), or all transforms on torch's current stream (identical "
+                         "transforms then run batched, one launch per stage for up to 8)")
     ap.add_argument("--timing", action="store_true", help="print the native timing tree")
     ap.add_argument("--check", action="store_true",
                     help="after timing: round-trip error on every rank and, on one rank, the "
@@ -148,8 +152,9 @@ def main():
     plane = grid.data_plane if world > 1 else "none"
     streams = []
     if a.sync == "stream":
-        if T == 1:
-            t.set_stream(torch.cuda.current_stream(), synchronous=False)
+        if T == 1 or a.streams == "one":
+            for tr in ts:
+                tr.set_stream(torch.cuda.current_stream(), synchronous=False)
         else:
             streams = [torch.cuda.Stream() for _ in range(T)]
             for tr, st in zip(ts, streams):
@@ -242,6 +247,7 @@ def main():
                 "distinct_devices": n_devices,
                 "shared_device": n_devices < world,
                 "sync": a.sync,
+                "streams": a.streams if T > 1 else "one",
                 "check_error": check,
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),

@@ -24,6 +24,29 @@ void check_distinct_grids(const std::vector<TransformImpl<T>*>& ts) {
   }
 }
 
+// Batched groups (GpuExecutor::backward_batch / forward_batch): GPU transforms
+// that can share launches, grouped by plan key in call order, at most
+// dev::kMaxBatch per group. Returns, per transform, whether a batch ran it.
+template <typename T, class Eligible, class Run>
+std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible eligible, Run run) {
+  const int n = static_cast<int>(ts.size());
+  std::vector<bool> done(n, false);
+  for (int i = 0; i < n; ++i) {
+    if (done[i] || !ts[i]->is_gpu() || !ts[i]->gpu()->batchable() || !eligible(i)) continue;
+    std::vector<int> group{i};
+    const auto key = ts[i]->gpu()->batch_key();
+    for (int j = i + 1; j < n && static_cast<int>(group.size()) < dev::kMaxBatch; ++j)
+      if (!done[j] && ts[j]->is_gpu() && ts[j]->gpu()->batchable() &&
+          ts[j]->gpu()->batch_key() == key && ts[j]->gpu()->batch_joinable(*ts[i]->gpu()) &&
+          eligible(j))
+        group.push_back(j);
+    if (group.size() < 2) continue;
+    run(group);
+    for (int j : group) done[j] = true;
+  }
+  return done;
+}
+
 template <typename T>
 void multi_forward(const std::vector<TransformImpl<T>*>& ts,
                    const SpfftProcessingUnitType* inputLocations, T* const* outputs,
@@ -32,14 +55,32 @@ void multi_forward(const std::vector<TransformImpl<T>*>& ts,
   check_distinct_grids(ts);
   const int n = static_cast<int>(ts.size());
   for (int i = 0; i < n; ++i)
-    if (ts[i]->is_gpu()) ts[i]->forward_xy(inputLocations[i]);
+    if (scalings[i] != SPFFT_NO_SCALING && scalings[i] != SPFFT_FULL_SCALING)
+      throw InvalidParameterError();
+  const std::vector<bool> batched = run_batches<T>(
+      ts,
+      [&](int i) {
+        return inputLocations[i] == SPFFT_PU_GPU && scalings[i] == scalings[0] &&
+               (ts[i]->plan().numLocalElements == 0 || is_device_pointer(outputs[i]));
+      },
+      [&](const std::vector<int>& g) {
+        std::vector<GpuExecutor<T>*> ex;
+        std::vector<T*> outs;
+        for (int j : g) {
+          ex.push_back(ts[j]->gpu());
+          outs.push_back(outputs[j]);
+        }
+        GpuExecutor<T>::forward_batch(ex, outs, scalings[g[0]]);
+      });
+  for (int i = 0; i < n; ++i)
+    if (ts[i]->is_gpu() && !batched[i]) ts[i]->forward_xy(inputLocations[i]);
   for (int i = 0; i < n; ++i)
     if (!ts[i]->is_gpu()) {
       ts[i]->forward_xy(inputLocations[i]);
       ts[i]->forward_exchange(true);
     }
   for (int i = 0; i < n; ++i)
-    if (ts[i]->is_gpu()) {
+    if (ts[i]->is_gpu() && !batched[i]) {
       ts[i]->forward_exchange(true);
       ts[i]->forward_z(outputs[i], scalings[i]);
     }
@@ -55,15 +96,30 @@ void multi_backward(const std::vector<TransformImpl<T>*>& ts, const T* const* in
   SPFFT_TIMED_SCOPE("multi_backward");
   check_distinct_grids(ts);
   const int n = static_cast<int>(ts.size());
+  const std::vector<bool> batched = run_batches<T>(
+      ts,
+      [&](int i) {
+        return outputLocations[i] == SPFFT_PU_GPU &&
+               (ts[i]->plan().numLocalElements == 0 || is_device_pointer(inputs[i]));
+      },
+      [&](const std::vector<int>& g) {
+        std::vector<GpuExecutor<T>*> ex;
+        std::vector<const T*> ins;
+        for (int j : g) {
+          ex.push_back(ts[j]->gpu());
+          ins.push_back(inputs[j]);
+        }
+        GpuExecutor<T>::backward_batch(ex, ins);
+      });
   for (int i = 0; i < n; ++i)
-    if (ts[i]->is_gpu()) ts[i]->backward_z(inputs[i]);
+    if (ts[i]->is_gpu() && !batched[i]) ts[i]->backward_z(inputs[i]);
   for (int i = 0; i < n; ++i)
     if (!ts[i]->is_gpu()) {
       ts[i]->backward_z(inputs[i]);
       ts[i]->backward_exchange(true);
     }
   for (int i = 0; i < n; ++i)
-    if (ts[i]->is_gpu()) {
+    if (ts[i]->is_gpu() && !batched[i]) {
       ts[i]->backward_exchange(true);
       ts[i]->backward_xy(outputLocations[i]);
     }

@@ -97,6 +97,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(twZ_, make_twiddles<T>(p.dimZ));
 
   if (!distributed) setup_fused();
+  batchEnabled_ = env_int("SPFFT_BATCH", 1, 0, 1) != 0;
+  compute_batch_key();
 
   if (distributed) {
     const std::int64_t eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
@@ -1089,6 +1091,148 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
                              hipMemcpyDeviceToHost, stream_),
               "hipMemcpyAsync");
   }
+}
+
+// ------------------------------------------------------- batched multi-transform
+namespace {
+struct Fnv {
+  std::uint64_t h = 1469598103934665603ull;
+  void bytes(const void* p, std::size_t n) {
+    const unsigned char* c = static_cast<const unsigned char*>(p);
+    for (std::size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  }
+  template <typename U>
+  void value(const U& v) { bytes(&v, sizeof(U)); }
+  template <typename U>
+  void vec(const std::vector<U>& v) {
+    value(v.size());
+    if (!v.empty()) bytes(v.data(), v.size() * sizeof(U));
+  }
+};
+}  // namespace
+
+// Everything the stage kernels read besides the data buffers: two transforms
+// with equal keys can share one launch (and the first one's device tables).
+template <typename T>
+void GpuExecutor<T>::compute_batch_key() {
+  const IndexPlan& p = *plan_;
+  Fnv f;
+  for (int v : {static_cast<int>(p.type), p.dimX, p.dimY, p.dimZ, p.numLocalElements, p.zeroStick,
+                p.colOfX0, deviceId_, interLayout_, static_cast<int>(sizeof(T))})
+    f.value(v);
+  f.value(interStride_);
+  f.vec(layout_.stickStride);
+  f.vec(layout_.colEntryBase);
+  f.value(layout_.slabStride);
+  f.value(twXh_ != nullptr);
+  f.vec(p.runs);
+  f.vec(p.stickRunOffsets);
+  f.vec(p.colX);
+  f.vec(p.colOffsets);
+  f.vec(p.colY);
+  batchKey_ = f.h | 1;  // never 0
+}
+
+template <typename T>
+bool GpuExecutor<T>::batchable() const {
+  return batchEnabled_ && plan_->size == 1 && !fused_ && !peerWrites_ && exchChunks_ <= 1 &&
+         chunkPlanes_ == 0 && !interRing_ && !capturing_ && !poison_;
+}
+
+// Members of a batch need no stream join: they either run on the leader's
+// stream, or all use their private streams synchronously, which are idle when
+// a call starts (the previous call ended with a stream synchronize) and are
+// synchronized again by multi_transform (the leader's covers the batch).
+// Cross-stream event joins were measured to cost more than the launches a
+// batch saves (profiles/r2_s3/batch_ab.txt).
+template <typename T>
+bool GpuExecutor<T>::batch_joinable(const GpuExecutor& leader) const {
+  if (stream_ == leader.stream_) return true;
+  return ownStreamActive_ && synchronous_ && leader.ownStreamActive_ && leader.synchronous_;
+}
+
+template <typename T>
+void GpuExecutor<T>::backward_batch(const std::vector<GpuExecutor*>& ex,
+                                    const std::vector<const T*>& inputs) {
+  SPFFT_TIMED_SCOPE("gpu_backward_batch");
+  const int n = static_cast<int>(ex.size());
+  if (n < 1 || n > dev::kMaxBatch || inputs.size() != ex.size()) throw InternalError();
+  GpuExecutor* l = ex[0];
+  DeviceGuard guard(l->deviceId_);
+  for (GpuExecutor* e : ex)
+    if (!e->batchable() || e->batchKey_ != l->batchKey_ || !e->batch_joinable(*l)) throw InternalError();
+  l->order_after_default_stream();
+  const IndexPlan& p = *l->plan_;
+  dev::BatchPtrs zb{}, yb{}, xb{};
+  zb.count = yb.count = xb.count = n;
+  for (int i = 0; i < n; ++i) {
+    GpuExecutor* e = ex[i];
+    if (p.numLocalElements > 0 && (!inputs[i] || !is_device_pointer(inputs[i])))
+      throw InvalidParameterError();
+    zb.in[i] = inputs[i];
+    zb.out[i] = e->grid_->device_slot(GridImpl<T>::kStickSide);
+    yb.in[i] = e->grid_->device_slot(GridImpl<T>::kSlabSide);
+    yb.out[i] = e->grid_->device_slot(GridImpl<T>::kInter);
+    xb.in[i] = yb.out[i];
+    xb.out[i] = e->grid_->device_slot(GridImpl<T>::kSpace);
+  }
+  auto za = l->zargs();
+  auto ya = l->yargs();
+  auto xa = l->xargs();
+  za.batch = zb;
+  ya.batch = yb;
+  xa.batch = xb;
+  hipStream_t s = l->stream_;
+  dev::launch_z_backward<T, cx<T>>(za, static_cast<const cx<T>*>(zb.in[0]),
+                                   static_cast<cx<T>*>(zb.out[0]), l->twZ_->data<cx<T>>(), s);
+  dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(yb.in[0]),
+                                   static_cast<cx<T>*>(yb.out[0]), l->twY_->data<cx<T>>(), s);
+  dev::launch_x_backward<T>(xa, p.type == SPFFT_TRANS_R2C, static_cast<const cx<T>*>(xb.in[0]),
+                            xb.out[0], l->twX_->data<cx<T>>(),
+                            l->twXh_ ? l->twXh_->data<cx<T>>() : nullptr, s);
+}
+
+template <typename T>
+void GpuExecutor<T>::forward_batch(const std::vector<GpuExecutor*>& ex, const std::vector<T*>& outputs,
+                                   SpfftScalingType scaling) {
+  SPFFT_TIMED_SCOPE("gpu_forward_batch");
+  const int n = static_cast<int>(ex.size());
+  if (n < 1 || n > dev::kMaxBatch || outputs.size() != ex.size()) throw InternalError();
+  GpuExecutor* l = ex[0];
+  DeviceGuard guard(l->deviceId_);
+  for (GpuExecutor* e : ex)
+    if (!e->batchable() || e->batchKey_ != l->batchKey_ || !e->batch_joinable(*l)) throw InternalError();
+  l->order_after_default_stream();
+  const IndexPlan& p = *l->plan_;
+  const T factor = scaling == SPFFT_FULL_SCALING
+                       ? static_cast<T>(1.0 / (static_cast<double>(p.dimX) * p.dimY * p.dimZ))
+                       : T(1);
+  dev::BatchPtrs zb{}, yb{}, xb{};
+  zb.count = yb.count = xb.count = n;
+  for (int i = 0; i < n; ++i) {
+    GpuExecutor* e = ex[i];
+    if (p.numLocalElements > 0 && (!outputs[i] || !is_device_pointer(outputs[i])))
+      throw InvalidParameterError();
+    xb.in[i] = e->grid_->device_slot(GridImpl<T>::kSpace);
+    xb.out[i] = e->grid_->device_slot(GridImpl<T>::kInter);
+    yb.in[i] = xb.out[i];
+    yb.out[i] = e->grid_->device_slot(GridImpl<T>::kSlabSide);
+    zb.in[i] = e->grid_->device_slot(GridImpl<T>::kStickSide);
+    zb.out[i] = outputs[i];
+  }
+  auto za = l->zargs();
+  auto ya = l->yargs();
+  auto xa = l->xargs();
+  za.batch = zb;
+  ya.batch = yb;
+  xa.batch = xb;
+  hipStream_t s = l->stream_;
+  dev::launch_x_forward<T>(xa, p.type == SPFFT_TRANS_R2C, xb.in[0], static_cast<cx<T>*>(xb.out[0]),
+                           l->twX_->data<cx<T>>(), l->twXh_ ? l->twXh_->data<cx<T>>() : nullptr, s);
+  dev::launch_y_forward<T, cx<T>>(ya, static_cast<const cx<T>*>(yb.in[0]),
+                                  static_cast<cx<T>*>(yb.out[0]), l->twY_->data<cx<T>>(), s);
+  dev::launch_z_forward<T, cx<T>>(za, static_cast<const cx<T>*>(zb.in[0]),
+                                  static_cast<cx<T>*>(zb.out[0]), factor, l->twZ_->data<cx<T>>(), s);
 }
 
 template class GpuExecutor<double>;

@@ -6,6 +6,7 @@
 // SpFFT contract) or never (asynchronous mode with a user stream).
 #pragma once
 
+#include <cstdint>
 #include <memory>
 #include <vector>
 
@@ -37,6 +38,21 @@ public:
   // the step-wise path. Opt-in with SPFFT_GRAPH=1.
   bool backward_graph(const T* input, SpfftProcessingUnitType outputLocation);
   bool forward_graph(SpfftProcessingUnitType inputLocation, T* output, SpfftScalingType scaling);
+
+  // Batched multi-transform: single-rank transforms on one device whose plans
+  // are identical (same dimensions, type, index set and layout knobs: equal
+  // batch_key()) run each stage of a direction as ONE launch for up to
+  // dev::kMaxBatch transforms (blockIdx.z = transform). Small grids are
+  // latency bound per launch; a batch fills the GPU (SPFFT_BATCH=0 disables).
+  // The batch runs on ex[0]'s stream: members share it, or all run on their
+  // private streams synchronously (batch_joinable). Inputs/outputs must be
+  // device pointers.
+  bool batchable() const;
+  bool batch_joinable(const GpuExecutor& leader) const;
+  std::uint64_t batch_key() const { return batchKey_; }
+  static void backward_batch(const std::vector<GpuExecutor*>& ex, const std::vector<const T*>& inputs);
+  static void forward_batch(const std::vector<GpuExecutor*>& ex, const std::vector<T*>& outputs,
+                            SpfftScalingType scaling);
 
   void synchronize();
   bool synchronous() const { return synchronous_; }
@@ -96,6 +112,9 @@ private:
   bool ownStreamActive_ = true;
   bool synchronous_ = true;
   std::unique_ptr<GpuEvent> event_;
+  std::uint64_t batchKey_ = 0;
+  bool batchEnabled_ = true;
+  void compute_batch_key();
   bool capturing_ = false;      // order/poison steps are skipped inside a capture
   bool graphsEnabled_ = false;  // SPFFT_GRAPH=1; off again after a failed capture
   bool warm_[2] = {false, false};  // first call of a direction runs eagerly

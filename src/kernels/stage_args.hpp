@@ -21,6 +21,17 @@
 namespace spfft {
 namespace dev {
 
+// Batched launches (multi_transform of transforms with identical plans on one
+// GPU): blockIdx.z selects the transform; its input and output buffers come
+// from these tables, every index table is shared. count <= 1: unbatched, the
+// kernel's pointer arguments are used as given.
+constexpr int kMaxBatch = 8;
+struct BatchPtrs {
+  int count;
+  const void* in[kMaxBatch];
+  void* out[kMaxBatch];
+};
+
 struct ZArgs {
   int numSticks;   // end of the stick range processed (exclusive)
   int stickBegin;  // first stick of the range (exchange pipelining chunks)
@@ -36,6 +47,7 @@ struct ZArgs {
   const long long* segStride;
   const int* segZOff;
   int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
+  BatchPtrs batch;
 };
 
 
@@ -78,6 +90,7 @@ struct YArgs {
   const ColDesc* colDesc;
   long long colStride;
   int remote;  // forward stores reach peers' memory: release system-wide at exit
+  BatchPtrs batch;
 };
 
 struct XArgs {
@@ -90,7 +103,11 @@ struct XArgs {
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
   long long interZStride, interBStride, interCStride;  // as YArgs
   const int* colX;
+  BatchPtrs batch;
 };
+
+// grid z extent of a launch (1 when unbatched)
+inline unsigned batch_dim(const BatchPtrs& b) { return b.count > 1 ? static_cast<unsigned>(b.count) : 1u; }
 
 // Engine geometry for diagnostics (SPFFT_LOG).
 std::string describe_engine(int n, bool dbl, bool lineFast);

@@ -645,12 +645,22 @@ __device__ __forceinline__ int tile_order(int t, int n) {
   return (SPFFT_REVERSE_READS & Bit) ? n - 1 - t : t;
 }
 
+// Batched launch (ZArgs/YArgs/XArgs::batch): the workgroup's transform
+// (blockIdx.z) supplies the input and output buffers; the index tables are
+// shared by every transform of the batch.
+#define SPFFT_BATCH_SELECT(a, IN, OUT)                                   \
+  if ((a).batch.count > 1) {                                           \
+    IN = static_cast<decltype(IN)>((a).batch.in[blockIdx.z]);          \
+    OUT = static_cast<decltype(OUT)>((a).batch.out[blockIdx.z]);       \
+  }
+
 // ---------------------------------------------------------------- z stage
 template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values, BT* __restrict__ out,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, values, out);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
   zero_lds(lds, eng.input_elems());
@@ -702,6 +712,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                      T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
   const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
@@ -751,6 +762,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, values, out);
   const int B = eng.lines();
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
@@ -794,6 +806,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                           T scale, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
   const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
   const int nl = min(B, a.numSticks - s0);
@@ -849,8 +862,8 @@ __device__ __forceinline__ int y_tile_zblock() {
   block_tile(bx, by);
   return SPFFT_Y_ZFAST ? bx : by;
 }
-inline dim3 y_grid(int cols, int zblocks) {
-  return SPFFT_Y_ZFAST ? dim3(zblocks, cols) : dim3(cols, zblocks);
+inline dim3 y_grid(int cols, int zblocks, unsigned batch = 1) {
+  return SPFFT_Y_ZFAST ? dim3(zblocks, cols, batch) : dim3(cols, zblocks, batch);
 }
 
 // ---------------------------------------------------------------- y stage
@@ -929,6 +942,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, in, inter);
   const int B = eng.lines();
   const int n = eng.n();
   const int c = a.colBegin + tile_order<1>(y_tile_col(), SPFFT_Y_ZFAST ? gridDim.y : gridDim.x);
@@ -988,6 +1002,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     y_forward_kernel(Eng eng, YArgs a, const cx<T>* __restrict__ inter, BT* __restrict__ out,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, inter, out);
   const int B = eng.lines();
   const int n = eng.n();
   const int c = a.colBegin + y_tile_col();
@@ -1045,6 +1060,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     x_backward_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, void* __restrict__ space,
                       const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, inter, space);
   const int B = eng.lines();
   const int n = eng.n();
   int tx, ty;
@@ -1085,6 +1101,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     x_forward_kernel(Eng eng, XArgs a, const void* __restrict__ space, cx<T>* __restrict__ inter,
                      const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, space, inter);
   const int B = eng.lines();
   const int n = eng.n();
   int tx, ty;
@@ -1127,6 +1144,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     x_backward_c2r_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, T* __restrict__ space,
                           const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, inter, space);
   const int B = eng.lines();
   const int h = eng.n();
   const long long n = 2 * static_cast<long long>(h);
@@ -1211,6 +1229,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     x_forward_r2c_kernel(Eng eng, XArgs a, const T* __restrict__ space, cx<T>* __restrict__ inter,
                          const cx<T>* __restrict__ twh, const cx<T>* __restrict__ twn) {
   SPFFT_LDS_DECL(T);
+  SPFFT_BATCH_SELECT(a, space, inter);
   const int B = eng.lines();
   const int h = eng.n();
   const long long n = 2 * static_cast<long long>(h);

@@ -24,7 +24,7 @@ void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space
       const std::size_t ldsTotal =
           lds + std::size_t(lines) * sizeof(cx<T>) + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
       prepare_kernel(k, ldsTotal);
-      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal,
+      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal,
                          stream, eng, a, inter, static_cast<T*>(space), twHalf, tw);
       gpu_check_launch("x_backward_c2r", stream);
     });
@@ -34,7 +34,7 @@ void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space
     auto k = r2c ? x_backward_kernel<decltype(eng), T, true> : x_backward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        inter, space, tw);
     gpu_check_launch("x_backward", stream);
   });

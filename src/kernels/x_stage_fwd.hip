@@ -21,7 +21,7 @@ void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
       auto k = x_forward_r2c_kernel<decltype(eng), T>;
       const std::size_t ldsTotal = lds + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
       prepare_kernel(k, ldsTotal);
-      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal,
+      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal,
                          stream, eng, a, static_cast<const T*>(space), inter, twHalf, tw);
       gpu_check_launch("x_forward_r2c", stream);
     });
@@ -31,7 +31,7 @@ void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
     auto k = r2c ? x_forward_kernel<decltype(eng), T, true> : x_forward_kernel<decltype(eng), T, false>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        space, inter, tw);
     gpu_check_launch("x_forward", stream);
   });

@@ -12,7 +12,7 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
     auto k = y_backward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines), batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        in, inter, tw);
     gpu_check_launch("y_backward", stream);
   });

@@ -13,7 +13,7 @@ void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* 
     auto k = y_forward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + std::size_t(a.n) * (sizeof(long long) + sizeof(int)) + 16;
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines), batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        inter, out, tw);
     gpu_check_launch("y_forward", stream);
   });

@@ -14,7 +14,7 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
                     : z_backward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        values, out, tw);
     gpu_check_launch("z_backward", stream);
   });

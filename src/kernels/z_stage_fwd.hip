@@ -14,7 +14,7 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
                     : z_forward_kernel<decltype(eng), T, BT>;
     const std::size_t ldsTotal = lds + run_table_bytes(lines);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        in, values, scale, tw);
     gpu_check_launch("z_forward", stream);
   });

@@ -297,6 +297,84 @@ def test_multi_transform_gpu(gpu):
         sp.multi_transform_backward([t0, t0], [vals[0], vals[0]])
 
 
+@pytest.mark.parametrize("ttype,single", [("C2C", False), ("R2C", False), ("C2C", True),
+                                           ("R2C", True)])
+@pytest.mark.parametrize("dims", [(32, 24, 20), (64, 64, 64)])
+def test_multi_transform_batched(gpu, ttype, single, dims):
+    """Batched multi_transform: transforms with identical plans share one launch per
+    stage (blockIdx.z = transform, groups of at most 8). 10 clones (a batch of 8 and one
+    of 2) plus a transform with another index set (unbatched path) in the middle; every
+    result equals the one-at-a-time result of a separate transform."""
+    import torch
+    rng = np.random.default_rng(21)
+    tt = getattr(sp.TransformType, ttype)
+    r2c = tt == sp.TransformType.R2C
+    nx, ny, nz = dims
+    GridCls = sp.GridFloat if single else sp.Grid
+    idx = sphere_indices(*dims, 0.5, r2c=r2c)
+    idx_o = sphere_indices(*dims, 0.3, r2c=r2c)
+
+    def make(ix):
+        g = GridCls(nx, ny, nz, nx * ny, GPU, 1)
+        return g, g.create_transform(GPU, tt, nx, ny, nz, nz, ix)
+
+    g0, t0 = make(idx)
+    go, to = make(idx_o)
+    ts = [t0] + [t0.clone() for _ in range(9)]
+    ts.insert(5, to)
+    vals = [torch.as_tensor(_rand_vals(rng, len(idx_o if t is to else idx), single), device=gpu)
+            for t in ts]
+    sp.timing_reset()
+    sp.timing_enable(True)
+    try:
+        spaces = [s.clone() for s in sp.multi_transform_backward(ts, vals)]
+        outs = sp.multi_transform_forward(ts, scalings=[sp.Scaling.FULL] * len(ts))
+        torch.cuda.synchronize()
+        rep = sp.timing_report()
+    finally:
+        sp.timing_enable(False)
+    assert "gpu_backward_batch" in rep and "gpu_forward_batch" in rep, rep
+    _, ref = make(idx)
+    _, ref_o = make(idx_o)
+    tol = 1e-5 if single else 1e-13
+    for t, v, s, o in zip(ts, vals, spaces, outs):
+        r = ref_o if t is to else ref
+        rs = r.backward(v).clone()
+        ro = r.forward(None, scaling=sp.Scaling.FULL)
+        assert max_rel_error(s.cpu().numpy(), rs.cpu().numpy()) <= tol
+        assert max_rel_error(o.cpu().numpy(), ro.cpu().numpy()) <= tol
+        if not r2c:
+            ix = idx_o if t is to else idx
+            ref_space = dense_backward(ix, v.cpu().numpy().astype(np.complex128), dims)
+            assert max_rel_error(s.cpu().numpy(), ref_space) < (1e-4 if single else 1e-12)
+            assert max_rel_error(o.cpu().numpy(), v.cpu().numpy()) < (1e-4 if single else 1e-12)
+
+
+def test_multi_transform_batch_disabled(gpu, monkeypatch):
+    """SPFFT_BATCH=0 (read at transform creation) keeps every transform on its own
+    launches; results are unchanged."""
+    import torch
+    monkeypatch.setenv("SPFFT_BATCH", "0")
+    rng = np.random.default_rng(22)
+    dims = (32, 32, 32)
+    idx = sphere_indices(*dims, 0.5)
+    grid = sp.Grid(*dims, 32 * 32, GPU, 1)
+    t0 = grid.create_transform(GPU, sp.TransformType.C2C, *dims, 32, idx)
+    ts = [t0, t0.clone()]
+    vals = [torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu) for _ in ts]
+    sp.timing_reset()
+    sp.timing_enable(True)
+    try:
+        outs = [s.clone() for s in sp.multi_transform_backward(ts, vals)]
+        torch.cuda.synchronize()
+        rep = sp.timing_report()
+    finally:
+        sp.timing_enable(False)
+    assert "gpu_backward_batch" not in rep
+    for o, v in zip(outs, vals):
+        assert max_rel_error(o.cpu().numpy(), dense_backward(idx, v.cpu().numpy(), dims)) < 1e-12
+
+
 def test_user_stream_async(gpu):
     import torch
     rng = np.random.default_rng(13)
