@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -31,16 +32,38 @@ inline void nccl_check(ncclResult_t r) {
 
 class RcclDeviceComm : public DeviceComm {
 public:
-  RcclDeviceComm(const std::shared_ptr<Communicator>& comm, int device)
+  // Collective on comm. Never throws between the collectives, so every rank
+  // takes part in both allgathers; ok() tells whether this rank's RCCL
+  // communicator came up (DeviceComm::create agrees on the outcome).
+  RcclDeviceComm(const std::shared_ptr<Communicator>& comm, int device, bool faultInit)
       : comm_(comm), rank_(comm->rank()), size_(comm->size()) {
     DeviceGuard guard(device);
-    ncclUniqueId id;
-    std::memset(&id, 0, sizeof(id));
-    if (rank_ == 0) nccl_check(ncclGetUniqueId(&id));
-    std::vector<ncclUniqueId> all(size_);
-    comm_->allgather(&id, all.data(), sizeof(id));
-    nccl_check(ncclCommInitRank(&nccl_, size_, all[0], rank_));
+    struct IdMsg {
+      ncclUniqueId id;
+      int ok;
+    };
+    IdMsg mine;
+    std::memset(&mine, 0, sizeof(mine));
+    mine.ok = 1;
+    if (rank_ == 0 && ncclGetUniqueId(&mine.id) != ncclSuccess) mine.ok = 0;
+    std::vector<IdMsg> all(size_);
+    comm_->allgather(&mine, all.data(), sizeof(IdMsg));
+    if (!all[0].ok) {
+      detail_ = "RCCL: ncclGetUniqueId failed on rank 0";
+      return;
+    }
+    if (faultInit) {  // fault injection (SPFFT_FAULT_RCCL_INIT=1 on every rank)
+      detail_ = "RCCL: initialisation failure injected (SPFFT_FAULT_RCCL_INIT)";
+      return;
+    }
+    const ncclResult_t r = ncclCommInitRank(&nccl_, size_, all[0].id, rank_);
+    if (r != ncclSuccess) {
+      detail_ = std::string("RCCL: ncclCommInitRank: ") + ncclGetErrorString(r);
+      nccl_ = nullptr;
+    }
   }
+  bool ok() const { return nccl_ != nullptr; }
+  const std::string& detail() const { return detail_; }
   ~RcclDeviceComm() override {
     if (nccl_ && !process_exiting()) (void)ncclCommDestroy(nccl_);
   }
@@ -99,6 +122,7 @@ private:
   int rank_, size_;
   ncclComm_t nccl_ = nullptr;
   bool aborted_ = false;
+  std::string detail_;
 };
 
 class LoopbackDeviceComm : public DeviceComm {
@@ -347,9 +371,33 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
                                       all[q].bus == all[r].bus && all[q].device == all[r].device);
   }
   const int prefer = all[0].prefer;
-  const bool peer = oneNode && prefer != 1 && (unbuffered || sharedDevice || prefer == 2);
+  // fault injection for the fallback below: every rank's RCCL initialisation
+  // reports failure (ranks sharing a device then try RCCL first as well)
+  const char* fenv = std::getenv("SPFFT_FAULT_RCCL_INIT");
+  const bool faultInit = fenv && std::atoi(fenv) != 0;
+  const bool peer =
+      oneNode && prefer != 1 && (unbuffered || (sharedDevice && !faultInit) || prefer == 2);
   if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, true));
-  return std::unique_ptr<DeviceComm>(new RcclDeviceComm(comm, device));
+  std::unique_ptr<RcclDeviceComm> rccl(new RcclDeviceComm(comm, device, faultInit));
+  // every rank learns whether every RCCL communicator came up
+  int ok = rccl->ok() ? 1 : 0;
+  std::vector<int> oks(P);
+  comm->allgather(&ok, oks.data(), sizeof(int));
+  bool allOk = true;
+  for (int v : oks) allOk = allOk && v != 0;
+  if (allOk) return std::unique_ptr<DeviceComm>(rccl.release());
+  const std::string why = rccl->ok() ? std::string("RCCL: another rank failed to initialise") : rccl->detail();
+  rccl->abort();
+  rccl.reset();
+  // one node: the peer-write data plane (IPC handles over xGMI) moves the data
+  // instead; across nodes there is no fallback
+  if (!oneNode || prefer == 1) {
+    set_error_detail(why);
+    throw MPIError();
+  }
+  if (comm->rank() == 0)
+    std::fprintf(stderr, "spfft: %s; using the peer-write (IPC) data plane\n", why.c_str());
+  return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, true));
 }
 
 }  // namespace spfft

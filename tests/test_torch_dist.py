@@ -61,6 +61,29 @@ def test_torch_dist_ipc_3ranks_repeated(gpu):
     _launch(3, "UNBUFFERED", "--iters=12", "--dims=64,60,48", expect="ipc")
 
 
+@pytest.mark.gpu
+def test_rccl_init_failure_falls_back_to_peer_writes(gpu, monkeypatch):
+    """Fault injection: every rank's RCCL initialisation fails. The ranks agree on
+    the outcome (allgather) and move the exchange with IPC peer writes instead."""
+    monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "1")
+    _launch(2, "COMPACT_BUFFERED", "--iters=2", expect="ipc")
+
+
+@pytest.mark.gpu
+def test_rccl_init_failure_strict(gpu, monkeypatch):
+    """With SPFFT_GPU_EXCHANGE=rccl there is no fallback: every rank raises MPIError
+    (with the cause) instead of hanging."""
+    monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "1")
+    monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", PROBE, "COMPACT_BUFFERED"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode != 0, out[-4000:]
+    assert "MPIError" in out and "SPFFT_FAULT_RCCL_INIT" in out, out[-4000:]
+
+
 def _bench_json(out):
     import json
     lines = [l for l in out.splitlines() if l.startswith("{") and '"metric"' in l]
