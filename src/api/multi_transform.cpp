@@ -4,6 +4,7 @@
 // GPU transforms each own a stream, so enqueuing stage k of every transform
 // before stage k+1 lets the GPU overlap transform i's exchange with transform
 // j's FFT kernels; host transforms run their stages in between.
+#include <algorithm>
 #include <set>
 #include <vector>
 
@@ -26,22 +27,33 @@ void check_distinct_grids(const std::vector<TransformImpl<T>*>& ts) {
 
 // Batched groups (GpuExecutor::backward_batch / forward_batch): GPU transforms
 // that can share launches, grouped by plan key in call order, at most
-// dev::kMaxBatch per group. Returns, per transform, whether a batch ran it.
+// dev::kMaxBatch per group; small grids batch join-free members only, large
+// grids run sub-batches of batch_split() on their leaders' streams. Returns,
+// per transform, whether a batch ran it.
 template <typename T, class Eligible, class Run>
 std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible eligible, Run run) {
   const int n = static_cast<int>(ts.size());
   std::vector<bool> done(n, false);
+  auto ok = [&](int j) {
+    return !done[j] && ts[j]->is_gpu() && ts[j]->gpu()->batchable() && eligible(j);
+  };
   for (int i = 0; i < n; ++i) {
-    if (done[i] || !ts[i]->is_gpu() || !ts[i]->gpu()->batchable() || !eligible(i)) continue;
+    if (!ok(i)) continue;
+    GpuExecutor<T>* lead = ts[i]->gpu();
+    const bool large = lead->batch_large();
     std::vector<int> group{i};
-    const auto key = ts[i]->gpu()->batch_key();
     for (int j = i + 1; j < n && static_cast<int>(group.size()) < dev::kMaxBatch; ++j)
-      if (!done[j] && ts[j]->is_gpu() && ts[j]->gpu()->batchable() &&
-          ts[j]->gpu()->batch_key() == key && ts[j]->gpu()->batch_joinable(*ts[i]->gpu()) &&
-          eligible(j))
+      if (ok(j) && ts[j]->gpu()->batch_key() == lead->batch_key() &&
+          (large || ts[j]->gpu()->batch_join_free(*lead)))
         group.push_back(j);
     if (group.size() < 2) continue;
-    run(group);
+    // sub-batches overlap only on different streams: one shared stream keeps one batch
+    bool oneStream = true;
+    for (int j : group) oneStream = oneStream && ts[j]->gpu()->stream() == lead->stream();
+    const std::size_t split =
+        large && !oneStream ? static_cast<std::size_t>(lead->batch_split()) : group.size();
+    for (std::size_t k = 0; k < group.size(); k += split)
+      run(std::vector<int>(group.begin() + k, group.begin() + std::min(group.size(), k + split)));
     for (int j : group) done[j] = true;
   }
   return done;

@@ -98,6 +98,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
 
   if (!distributed) setup_fused();
   batchEnabled_ = env_int("SPFFT_BATCH", 1, 0, 1) != 0;
+  batchLarge_ = env_int("SPFFT_BATCH_LARGE", 1 << 22, 0, std::numeric_limits<int>::max());
+  batchSplit_ = env_int("SPFFT_BATCH_SPLIT", 2, 1, dev::kMaxBatch);
   compute_batch_key();
 
   if (distributed) {
@@ -1139,16 +1141,56 @@ bool GpuExecutor<T>::batchable() const {
          chunkPlanes_ == 0 && !interRing_ && !capturing_ && !poison_;
 }
 
-// Members of a batch need no stream join: they either run on the leader's
-// stream, or all use their private streams synchronously, which are idle when
-// a call starts (the previous call ended with a stream synchronize) and are
+// A member needs no stream join when it runs on the leader's stream, or when
+// both use their private streams synchronously: those are idle when a call
+// starts (the previous call ended with a stream synchronize) and are
 // synchronized again by multi_transform (the leader's covers the batch).
-// Cross-stream event joins were measured to cost more than the launches a
-// batch saves (profiles/r2_s3/batch_ab.txt).
+// Event joins cost ~3.4 us of host time per hipStreamWaitEvent on ROCm 7.2,
+// more than the launches a batch saves on small grids
+// (profiles/r2_s3/batch_ab.txt).
 template <typename T>
-bool GpuExecutor<T>::batch_joinable(const GpuExecutor& leader) const {
+bool GpuExecutor<T>::batch_join_free(const GpuExecutor& leader) const {
   if (stream_ == leader.stream_) return true;
   return ownStreamActive_ && synchronous_ && leader.ownStreamActive_ && leader.synchronous_;
+}
+
+template <typename T>
+bool GpuExecutor<T>::batch_large() const {
+  const IndexPlan& p = *plan_;
+  return static_cast<long long>(p.dimX) * p.dimY * p.local_planes() >= batchLarge_;
+}
+
+// members on other streams: ordered after the default stream (private mode) and
+// after their own streams' earlier work, then the leader's stream runs the batch
+template <typename T>
+void GpuExecutor<T>::batch_join(const std::vector<GpuExecutor*>& ex) {
+  GpuExecutor* l = ex[0];
+  l->order_after_default_stream();
+  for (std::size_t i = 1; i < ex.size(); ++i) {
+    GpuExecutor* e = ex[i];
+    if (!e->batch_needs_join(*l)) continue;
+    e->order_after_default_stream();
+    if (!e->joinEvent_) e->joinEvent_.reset(new GpuEvent());
+    e->joinEvent_->record(e->stream_);
+    e->joinEvent_->wait_on(l->stream_);
+  }
+}
+
+// joined members' streams wait for the batch, so later work on them sees it
+template <typename T>
+void GpuExecutor<T>::batch_release(const std::vector<GpuExecutor*>& ex) {
+  GpuExecutor* l = ex[0];
+  bool recorded = false;
+  for (std::size_t i = 1; i < ex.size(); ++i) {
+    GpuExecutor* e = ex[i];
+    if (!e->batch_needs_join(*l)) continue;
+    if (!recorded) {
+      if (!l->doneEvent_) l->doneEvent_.reset(new GpuEvent());
+      l->doneEvent_->record(l->stream_);
+      recorded = true;
+    }
+    l->doneEvent_->wait_on(e->stream_);
+  }
 }
 
 template <typename T>
@@ -1160,8 +1202,8 @@ void GpuExecutor<T>::backward_batch(const std::vector<GpuExecutor*>& ex,
   GpuExecutor* l = ex[0];
   DeviceGuard guard(l->deviceId_);
   for (GpuExecutor* e : ex)
-    if (!e->batchable() || e->batchKey_ != l->batchKey_ || !e->batch_joinable(*l)) throw InternalError();
-  l->order_after_default_stream();
+    if (!e->batchable() || e->batchKey_ != l->batchKey_) throw InternalError();
+  batch_join(ex);
   const IndexPlan& p = *l->plan_;
   dev::BatchPtrs zb{}, yb{}, xb{};
   zb.count = yb.count = xb.count = n;
@@ -1190,6 +1232,7 @@ void GpuExecutor<T>::backward_batch(const std::vector<GpuExecutor*>& ex,
   dev::launch_x_backward<T>(xa, p.type == SPFFT_TRANS_R2C, static_cast<const cx<T>*>(xb.in[0]),
                             xb.out[0], l->twX_->data<cx<T>>(),
                             l->twXh_ ? l->twXh_->data<cx<T>>() : nullptr, s);
+  batch_release(ex);
 }
 
 template <typename T>
@@ -1201,8 +1244,8 @@ void GpuExecutor<T>::forward_batch(const std::vector<GpuExecutor*>& ex, const st
   GpuExecutor* l = ex[0];
   DeviceGuard guard(l->deviceId_);
   for (GpuExecutor* e : ex)
-    if (!e->batchable() || e->batchKey_ != l->batchKey_ || !e->batch_joinable(*l)) throw InternalError();
-  l->order_after_default_stream();
+    if (!e->batchable() || e->batchKey_ != l->batchKey_) throw InternalError();
+  batch_join(ex);
   const IndexPlan& p = *l->plan_;
   const T factor = scaling == SPFFT_FULL_SCALING
                        ? static_cast<T>(1.0 / (static_cast<double>(p.dimX) * p.dimY * p.dimZ))
@@ -1233,6 +1276,7 @@ void GpuExecutor<T>::forward_batch(const std::vector<GpuExecutor*>& ex, const st
                                   static_cast<cx<T>*>(yb.out[0]), l->twY_->data<cx<T>>(), s);
   dev::launch_z_forward<T, cx<T>>(za, static_cast<const cx<T>*>(zb.in[0]),
                                   static_cast<cx<T>*>(zb.out[0]), factor, l->twZ_->data<cx<T>>(), s);
+  batch_release(ex);
 }
 
 template class GpuExecutor<double>;

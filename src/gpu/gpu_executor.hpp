@@ -44,11 +44,16 @@ public:
   // batch_key()) run each stage of a direction as ONE launch for up to
   // dev::kMaxBatch transforms (blockIdx.z = transform). Small grids are
   // latency bound per launch; a batch fills the GPU (SPFFT_BATCH=0 disables).
-  // The batch runs on ex[0]'s stream: members share it, or all run on their
-  // private streams synchronously (batch_joinable). Inputs/outputs must be
-  // device pointers.
+  // The batch runs on ex[0]'s stream. Members on other streams are joined by
+  // events, which costs more host time than the saved launches on small grids:
+  // there only join-free members are batched (batch_join_free). Large grids
+  // (batch_large: GPU bound, the joins hide behind the kernels) are batched in
+  // sub-batches of batch_split() on their leaders' streams, so the stages of
+  // different sub-batches overlap. Inputs/outputs must be device pointers.
   bool batchable() const;
-  bool batch_joinable(const GpuExecutor& leader) const;
+  bool batch_join_free(const GpuExecutor& leader) const;
+  bool batch_large() const;
+  int batch_split() const { return batchSplit_; }
   std::uint64_t batch_key() const { return batchKey_; }
   static void backward_batch(const std::vector<GpuExecutor*>& ex, const std::vector<const T*>& inputs);
   static void forward_batch(const std::vector<GpuExecutor*>& ex, const std::vector<T*>& outputs,
@@ -114,6 +119,14 @@ private:
   std::unique_ptr<GpuEvent> event_;
   std::uint64_t batchKey_ = 0;
   bool batchEnabled_ = true;
+  long long batchLarge_ = 0;  // slab elements from which joins are allowed
+  int batchSplit_ = 2;        // sub-batch size of large grids
+  std::unique_ptr<GpuEvent> joinEvent_, doneEvent_;
+  static void batch_join(const std::vector<GpuExecutor*>& ex);
+  static void batch_release(const std::vector<GpuExecutor*>& ex);
+  bool batch_needs_join(const GpuExecutor& leader) const {
+    return stream_ != leader.stream_ && !batch_join_free(leader);
+  }
   void compute_batch_key();
   bool capturing_ = false;      // order/poison steps are skipped inside a capture
   bool graphsEnabled_ = false;  // SPFFT_GRAPH=1; off again after a failed capture

@@ -350,6 +350,46 @@ def test_multi_transform_batched(gpu, ttype, single, dims):
             assert max_rel_error(o.cpu().numpy(), v.cpu().numpy()) < (1e-4 if single else 1e-12)
 
 
+@pytest.mark.parametrize("split", ["2", "3"])
+def test_multi_transform_batched_streams(gpu, monkeypatch, split):
+    """Large-grid batching (SPFFT_BATCH_LARGE=0 makes every grid "large"): transforms on
+    their own async user streams run in sub-batches of SPFFT_BATCH_SPLIT on the
+    sub-batch leader's stream, joined to the members' streams by events; later work
+    on each member's stream sees the results."""
+    import torch
+    monkeypatch.setenv("SPFFT_BATCH_LARGE", "0")
+    monkeypatch.setenv("SPFFT_BATCH_SPLIT", split)
+    rng = np.random.default_rng(23)
+    dims = (48, 40, 36)
+    idx = sphere_indices(*dims, 0.5)
+    grid = sp.Grid(*dims, 48 * 40, GPU, 1)
+    t0 = grid.create_transform(GPU, sp.TransformType.C2C, *dims, 36, idx)
+    ts = [t0] + [t0.clone() for _ in range(4)]
+    streams = [torch.cuda.Stream() for _ in ts]
+    for t, st in zip(ts, streams):
+        t.set_stream(st, synchronous=False)
+    vals = [torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu) for _ in ts]
+    outs = [torch.empty_like(v) for v in vals]
+    sp.timing_reset()
+    sp.timing_enable(True)
+    try:
+        for _ in range(2):
+            spaces = sp.multi_transform_backward(ts, vals)
+            copies = []
+            for s_, st in zip(spaces, streams):
+                with torch.cuda.stream(st):  # ordered after the batch on each stream
+                    copies.append(s_.clone())
+            sp.multi_transform_forward(ts, outputs=outs, scalings=[sp.Scaling.FULL] * len(ts))
+        torch.cuda.synchronize()
+        rep = sp.timing_report()
+    finally:
+        sp.timing_enable(False)
+    assert "gpu_backward_batch" in rep and "gpu_forward_batch" in rep, rep
+    for c, o, v in zip(copies, outs, vals):
+        assert max_rel_error(c.cpu().numpy(), dense_backward(idx, v.cpu().numpy(), dims)) < 1e-12
+        assert max_rel_error(o.cpu().numpy(), v.cpu().numpy()) < 1e-12
+
+
 def test_multi_transform_batch_disabled(gpu, monkeypatch):
     """SPFFT_BATCH=0 (read at transform creation) keeps every transform on its own
     launches; results are unchanged."""
