@@ -100,6 +100,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   batchEnabled_ = env_int("SPFFT_BATCH", 1, 0, 1) != 0;
   batchLarge_ = env_int("SPFFT_BATCH_LARGE", 1 << 22, 0, std::numeric_limits<int>::max());
   batchSplit_ = env_int("SPFFT_BATCH_SPLIT", 2, 1, dev::kMaxBatch);
+  xySplit_ = env_int("SPFFT_XY_SPLIT", 0, 0, 1) != 0;
   compute_batch_key();
 
   if (distributed) {
@@ -935,8 +936,11 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   // plane chunks: the intermediate of a chunk is read back by the x stage while
   // it is still resident in the last-level (Infinity) cache
   const int L = plan_->local_planes();
-  const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
+  const bool split = xy_split_active();
+  const int chunk = split ? (L + 1) / 2 : (chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1));
+  if (split) xy_fork();
   for (int zb = 0; zb < L; zb += chunk) {
+    const hipStream_t s = split && zb > 0 ? helperStream_->get() : stream_;
     auto ya = yargs();
     auto xa = xargs();
     ya.zBegin = xa.zBegin = zb;
@@ -946,13 +950,14 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
         interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (floatExchange_)
       dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
-                                           twY_->data<cx<T>>(), stream_);
+                                           twY_->data<cx<T>>(), s);
     else
       dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
-                                       twY_->data<cx<T>>(), stream_);
+                                       twY_->data<cx<T>>(), s);
     dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space,
-                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, s);
   }
+  if (split) xy_join();
   if (outputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
                              hipMemcpyDeviceToHost, stream_),
@@ -1015,8 +1020,11 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
     return;
   }
   const int L = plan_->local_planes();
-  const int chunk = chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1);
+  const bool split = xy_split_active();
+  const int chunk = split ? (L + 1) / 2 : (chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1));
+  if (split) xy_fork();
   for (int zb = 0; zb < L; zb += chunk) {
+    const hipStream_t s = split && zb > 0 ? helperStream_->get() : stream_;
     auto ya = yargs();
     auto xa = xargs();
     ya.zBegin = xa.zBegin = zb;
@@ -1029,14 +1037,40 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       ya.remote = 1;
     }
     dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
-                             twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+                             twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, s);
     if (floatExchange_)
       dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
-                                          twY_->data<cx<T>>(), stream_);
+                                          twY_->data<cx<T>>(), s);
     else
       dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
-                                      stream_);
+                                      s);
   }
+  if (split) xy_join();
+}
+
+template <typename T>
+bool GpuExecutor<T>::xy_split_active() const {
+  return xySplit_ && plan_->size == 1 && !fused_ && chunkPlanes_ == 0 && !interRing_ &&
+         !capturing_ && plan_->local_planes() >= 2 && batch_large();
+}
+
+// the helper stream starts after the work queued so far on the execution stream
+template <typename T>
+void GpuExecutor<T>::xy_fork() {
+  if (!helperStream_) {
+    helperStream_.reset(new GpuStream());
+    forkEvent_.reset(new GpuEvent());
+    helperDone_.reset(new GpuEvent());
+  }
+  forkEvent_->record(stream_);
+  forkEvent_->wait_on(helperStream_->get());
+}
+
+// the execution stream continues after the helper stream's half
+template <typename T>
+void GpuExecutor<T>::xy_join() {
+  helperDone_->record(helperStream_->get());
+  helperDone_->wait_on(stream_);
 }
 
 template <typename T>

@@ -122,6 +122,16 @@ private:
   long long batchLarge_ = 0;  // slab elements from which joins are allowed
   int batchSplit_ = 2;        // sub-batch size of large grids
   std::unique_ptr<GpuEvent> joinEvent_, doneEvent_;
+  // Single-rank y/x stages split into two plane halves on two streams (fork /
+  // join by events), so one half's y stage overlaps the other's x stage and the
+  // kernel tails fill each other (SPFFT_XY_SPLIT=1; large grids only). Measured
+  // 4-8% slower at 256^3 (profiles/r2_s3/xy_split.txt): off by default.
+  bool xySplit_ = false;
+  std::unique_ptr<GpuStream> helperStream_;
+  std::unique_ptr<GpuEvent> forkEvent_, helperDone_;
+  bool xy_split_active() const;
+  void xy_fork();
+  void xy_join();
   static void batch_join(const std::vector<GpuExecutor*>& ex);
   static void batch_release(const std::vector<GpuExecutor*>& ex);
   bool batch_needs_join(const GpuExecutor& leader) const {
