@@ -148,7 +148,8 @@ bool has_ct_kernel(int n);
 #ifndef SPFFT_MR_SIZES
 #if SPFFT_MR
 #define SPFFT_MR_SIZES(X)                                                                 \
-  X(96) X(100) X(108) X(120) X(125) X(135) X(144) X(150) X(160) X(180) X(192) X(200) X(216) \
+  X(48) X(60) X(72) X(80) X(90) X(96) X(100) X(108) X(120) X(125) X(135) X(144) X(150) X(160) \
+  X(180) X(192) X(200) X(216) \
   X(240) X(288) X(320) X(360) X(384) \
   X(400) X(480)
 #else

@@ -196,7 +196,8 @@ def test_composite_radices(gpu, dims, ttype, single):
 
 @pytest.mark.parametrize("dims", [(240, 12, 10), (10, 200, 12), (12, 10, 192), (192, 240, 200),
                                   (96, 144, 216), (360, 8, 10), (6, 480, 8), (10, 6, 384),
-                                  (100, 108, 125), (150, 135, 12), (250, 10, 100)])
+                                  (100, 108, 125), (150, 135, 12), (250, 10, 100),
+                                  (48, 60, 72), (80, 90, 12), (180, 8, 60)])
 @pytest.mark.parametrize("ttype", ["c2c", "r2c"])
 @pytest.mark.parametrize("single", [False, True])
 def test_mixed_radix_ct_lengths(gpu, dims, ttype, single):
