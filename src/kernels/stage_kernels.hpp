@@ -933,6 +933,15 @@ struct ColEntries {
   }
 };
 
+// LDS the y-stage kernels reserve behind the FFT lines for ColEntries' list
+// mode (colBase, y -> entry, entry -> y). With column run descriptors only the
+// backward R2C x = 0 column (hermitian fill, list mode) needs it; C2C plans
+// skip it, which keeps fp32 N = 256 at 4 workgroups per CU instead of 3.
+inline std::size_t col_entries_lds(const YArgs& a, bool backward) {
+  const bool list = !a.colDesc || (backward && a.colOfX0 >= 0);
+  return list ? std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16 : 0;
+}
+
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
 // loads straight from the stick side — consecutive lanes read consecutive z
 // of one stick (coalesced) — with no LDS staging of the input. The x = 0
