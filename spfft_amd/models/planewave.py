@@ -74,21 +74,21 @@ class PlaneWaveBasis:
 class PlaneWaveModel:
     """Band-parallel local-potential and density operations on one device.
 
-    `num_streams` transforms (one Grid each) are used round-robin and overlap
-    through multi_transform."""
+    `num_transforms` transforms (one Grid each, identical plans: a transform and
+    its clones) process that many bands per multi_transform call. On the GPU
+    the library runs such a group batched, one launch per stage for up to 8
+    bands (multi_transform.cpp), so small grids are not launch bound."""
 
     def __init__(self, basis: PlaneWaveBasis, processing_unit=ProcessingUnit.GPU,
-                 num_transforms: int = 2, single: bool = False):
+                 num_transforms: int = 8, single: bool = False):
         from ..grid import Grid, GridFloat
         self.basis = basis
         self.pu = processing_unit
         n0, n1, n2 = basis.fft_dims
         cls = GridFloat if single else Grid
-        self.transforms = []
-        for _ in range(max(1, num_transforms)):
-            g = cls(n0, n1, n2, n0 * n1, processing_unit, -1)
-            self.transforms.append(g.create_transform(processing_unit, TransformType.C2C,
-                                                      n0, n1, n2, n2, basis.indices))
+        g = cls(n0, n1, n2, n0 * n1, processing_unit, -1)
+        t0 = g.create_transform(processing_unit, TransformType.C2C, n0, n1, n2, n2, basis.indices)
+        self.transforms = [t0] + [t0.clone() for _ in range(max(1, num_transforms) - 1)]
         self.volume_points = n0 * n1 * n2
 
     def apply_local_potential(self, psi: Sequence, v_r) -> List:
@@ -112,11 +112,16 @@ class PlaneWaveModel:
 
     def density(self, psi: Sequence, weights: Sequence[float]):
         """rho(r) = sum_b w_b |psi_b(r)|^2 on the real-space grid [z][y][x]."""
+        from ..grid import multi_transform_backward
         rho = None
-        for c, w in zip(psi, weights):
-            s = self.transforms[0].backward(c)
-            contrib = (s.real ** 2 + s.imag ** 2) * w
-            rho = contrib if rho is None else rho + contrib
+        T = len(self.transforms)
+        psi, weights = list(psi), list(weights)
+        for start in range(0, len(psi), T):
+            group = psi[start:start + T]
+            spaces = multi_transform_backward(self.transforms[:len(group)], group)
+            for s, w in zip(spaces, weights[start:start + T]):
+                contrib = (s.real ** 2 + s.imag ** 2) * w
+                rho = contrib if rho is None else rho + contrib
         return rho
 
     def kinetic(self, psi: Sequence) -> List:
