@@ -29,9 +29,11 @@ void check_distinct_grids(const std::vector<TransformImpl<T>*>& ts) {
 // that can share launches, grouped by plan key in call order, at most
 // dev::kMaxBatch per group; small grids batch join-free members only, large
 // grids run sub-batches of batch_split() on their leaders' streams. Returns,
-// per transform, whether a batch ran it.
-template <typename T, class Eligible, class Run>
-std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible eligible, Run run) {
+// per transform, whether a batch ran it. `tag(i)` must match within a group
+// (the forward scaling).
+template <typename T, class Eligible, class Tag, class Run>
+std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible eligible, Tag tag,
+                              Run run) {
   const int n = static_cast<int>(ts.size());
   std::vector<bool> done(n, false);
   auto ok = [&](int j) {
@@ -43,7 +45,7 @@ std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible
     const bool large = lead->batch_large();
     std::vector<int> group{i};
     for (int j = i + 1; j < n && static_cast<int>(group.size()) < dev::kMaxBatch; ++j)
-      if (ok(j) && ts[j]->gpu()->batch_key() == lead->batch_key() &&
+      if (ok(j) && ts[j]->gpu()->batch_key() == lead->batch_key() && tag(j) == tag(i) &&
           (large || ts[j]->gpu()->batch_join_free(*lead)))
         group.push_back(j);
     if (group.size() < 2) continue;
@@ -72,9 +74,10 @@ void multi_forward(const std::vector<TransformImpl<T>*>& ts,
   const std::vector<bool> batched = run_batches<T>(
       ts,
       [&](int i) {
-        return inputLocations[i] == SPFFT_PU_GPU && scalings[i] == scalings[0] &&
+        return inputLocations[i] == SPFFT_PU_GPU &&
                (ts[i]->plan().numLocalElements == 0 || is_device_pointer(outputs[i]));
       },
+      [&](int i) { return static_cast<int>(scalings[i]); },
       [&](const std::vector<int>& g) {
         std::vector<GpuExecutor<T>*> ex;
         std::vector<T*> outs;
@@ -114,6 +117,7 @@ void multi_backward(const std::vector<TransformImpl<T>*>& ts, const T* const* in
         return outputLocations[i] == SPFFT_PU_GPU &&
                (ts[i]->plan().numLocalElements == 0 || is_device_pointer(inputs[i]));
       },
+      [](int) { return 0; },
       [&](const std::vector<int>& g) {
         std::vector<GpuExecutor<T>*> ex;
         std::vector<const T*> ins;

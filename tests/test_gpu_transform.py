@@ -392,6 +392,26 @@ def test_multi_transform_batched_streams(gpu, monkeypatch, split):
         assert max_rel_error(o.cpu().numpy(), v.cpu().numpy()) < 1e-12
 
 
+def test_multi_transform_batched_mixed_scaling(gpu):
+    """Forward batches group transforms of equal scaling only ([NONE, FULL, FULL, NONE]
+    -> two batches); each output matches its scaling."""
+    import torch
+    rng = np.random.default_rng(24)
+    dims = (32, 32, 32)
+    idx = sphere_indices(*dims, 0.5)
+    grid = sp.Grid(*dims, 32 * 32, GPU, 1)
+    t0 = grid.create_transform(GPU, sp.TransformType.C2C, *dims, 32, idx)
+    ts = [t0] + [t0.clone() for _ in range(3)]
+    vals = [torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu) for _ in ts]
+    sp.multi_transform_backward(ts, vals)
+    sc = [sp.Scaling.NONE, sp.Scaling.FULL, sp.Scaling.FULL, sp.Scaling.NONE]
+    outs = sp.multi_transform_forward(ts, scalings=sc)
+    n = float(np.prod(dims))
+    for o, v, s_ in zip(outs, vals, sc):
+        ref = v.cpu().numpy() * (1.0 if s_ == sp.Scaling.FULL else n)
+        assert max_rel_error(o.cpu().numpy(), ref) < 1e-12
+
+
 def test_multi_transform_batch_disabled(gpu, monkeypatch):
     """SPFFT_BATCH=0 (read at transform creation) keeps every transform on its own
     launches; results are unchanged."""
