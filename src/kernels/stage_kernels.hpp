@@ -891,6 +891,12 @@ __device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride
 // Every kernel keeps a single FFT call site whichever source is used: the
 // run-time engines inline their whole pass switch per call site, and a second
 // copy doubled their register demand (profiles/r2_s1/rt_regression.txt).
+// SPFFT_Y_BASE_TABLE=1: descriptor columns also get a y -> base table in LDS
+// (experiment: trades ~30 VALU instructions of run selects per element for one
+// LDS read; see profiles/r2_s3/f32/)
+#ifndef SPFFT_Y_BASE_TABLE
+#define SPFFT_Y_BASE_TABLE 0
+#endif
 template <class Eng>
 struct ColEntries {
   bool useDesc;
@@ -910,6 +916,15 @@ struct ColEntries {
     ne = 0;
     if (useDesc) {
       d = a.colDesc[c];
+#if SPFFT_Y_BASE_TABLE
+      // y -> base (or -1) once per workgroup: one LDS read per element instead
+      // of the per-element run selects
+      for (int y = threadIdx.x; y < n; y += blockDim.x) {
+        long long b;
+        cBase[y] = col_desc_find(d, stride, y, b) ? b : -1;
+      }
+      __syncthreads();
+#endif
       return;
     }
     const int k0 = a.colOffsets[c];
@@ -926,7 +941,14 @@ struct ColEntries {
   }
   // whether the column has an entry at y; its base (add the plane) in base
   __device__ bool find(int y, long long& base) const {
+#if SPFFT_Y_BASE_TABLE
+    if (useDesc) {
+      base = cBase[y];
+      return base >= 0;
+    }
+#else
     if (useDesc) return col_desc_find(d, stride, y, base);
+#endif
     const int e = yEnt[y];
     base = e < 0 ? 0 : cBase[e];
     return e >= 0;
@@ -939,7 +961,8 @@ struct ColEntries {
 // skip it, which keeps fp32 N = 256 at 4 workgroups per CU instead of 3.
 inline std::size_t col_entries_lds(const YArgs& a, bool backward) {
   const bool list = !a.colDesc || (backward && a.colOfX0 >= 0);
-  return list ? std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16 : 0;
+  if (list) return std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
+  return SPFFT_Y_BASE_TABLE ? std::size_t(a.n) * sizeof(long long) + 16 : 0;
 }
 
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
