@@ -897,6 +897,7 @@ __device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride
 #ifndef SPFFT_Y_BASE_TABLE
 #define SPFFT_Y_BASE_TABLE 0
 #endif
+constexpr long long kNoBase = -0x7fffffffffffffffLL - 1;
 template <class Eng>
 struct ColEntries {
   bool useDesc;
@@ -919,9 +920,11 @@ struct ColEntries {
 #if SPFFT_Y_BASE_TABLE
       // y -> base (or -1) once per workgroup: one LDS read per element instead
       // of the per-element run selects
+      // miss sentinel LLONG_MIN: peer-write plans hold negative bases (offsets
+      // of a peer's buffer from the local one)
       for (int y = threadIdx.x; y < n; y += blockDim.x) {
         long long b;
-        cBase[y] = col_desc_find(d, stride, y, b) ? b : -1;
+        cBase[y] = col_desc_find(d, stride, y, b) ? b : kNoBase;
       }
       __syncthreads();
 #endif
@@ -944,7 +947,7 @@ struct ColEntries {
 #if SPFFT_Y_BASE_TABLE
     if (useDesc) {
       base = cBase[y];
-      return base >= 0;
+      return base != kNoBase;
     }
 #else
     if (useDesc) return col_desc_find(d, stride, y, base);
