@@ -58,10 +58,15 @@ SPFFT_EXPORT SpfftError spfft_amd_float_grid_create_distributed(
     SpfftAmdComm comm, SpfftExchangeType exchangeType);
 SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchangeType* type);
 /* GPU data plane of a distributed grid: "rccl", "ipc" (peer writes across
- * processes), "peer" (peer writes inside a local group), "loopback", or "none"
- * (local or host-only grid). Collective on first call (creates the data plane). */
+ * processes), "peer" (peer writes inside a local group), "loopback",
+ * "rccl-self" (local group moved by RCCL), or "none" (local or host-only
+ * grid). Collective on first call (creates the data plane). */
 SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name);
+/* Number of RCCL communicators this process has created. Grids whose
+ * communicators have the same members on the same devices share one
+ * (SPFFT_RCCL_SHARE=0: one per grid). */
+SPFFT_EXPORT SpfftError spfft_amd_rccl_communicators(int* count);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 

@@ -32,3 +32,15 @@ def device_count() -> int:
 def build_info() -> str:
     from .ops._lib import lib
     return lib().spfft_amd_build_info().decode()
+
+
+def rccl_communicators() -> int:
+    """RCCL communicators this process has created (grids with the same members on
+    the same devices share one)."""
+    import ctypes
+    from .ops._lib import lib
+    n = ctypes.c_int()
+    rc = lib().spfft_amd_rccl_communicators(ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"spfft_amd_rccl_communicators failed ({rc})")
+    return n.value

@@ -149,8 +149,8 @@ class _GridBase:
 
     @property
     def data_plane(self) -> str:
-        """GPU data plane of a distributed grid: "rccl", "ipc", "peer", "loopback" or
-        "none". Collective on first use (it creates the data plane)."""
+        """GPU data plane of a distributed grid: "rccl", "ipc", "peer", "loopback",
+        "rccl-self" or "none". Collective on first use (it creates the data plane)."""
         v = ctypes.c_char_p()
         _check(self._prec.amd_fn("grid_data_plane")(self._h, ctypes.byref(v)))
         return v.value.decode()

@@ -364,6 +364,12 @@ SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** nam
   return with_handle<GridFloat>(grid, [&](GridFloat& g) { *name = data_plane_of(*g.impl()); });
 }
 
+SpfftError spfft_amd_rccl_communicators(int* count) {
+  if (!count) return SPFFT_INVALID_PARAMETER_ERROR;
+  *count = spfft::DeviceComm::rccl_channels_created();
+  return SPFFT_SUCCESS;
+}
+
 SpfftError spfft_amd_transform_set_stream(SpfftTransform t, void* stream, int synchronous) {
   return with_handle<Transform>(
       t, [&](Transform& x) { x.set_execution_stream(stream, synchronous != 0); });

@@ -5,10 +5,15 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "core/common.hpp"
@@ -21,22 +26,61 @@ namespace spfft {
 
 DeviceComm::~DeviceComm() = default;
 
-namespace {
-
-inline void nccl_check(ncclResult_t r) {
-  if (r != ncclSuccess) {
-    set_error_detail(std::string("RCCL: ") + ncclGetErrorString(r) + " " + ncclGetLastError(nullptr));
-    throw MPIError();
-  }
+double comm_timeout_seconds() {
+  // default 120 s: a dead or missing peer becomes an MPIError instead of a hang;
+  // SPFFT_COMM_TIMEOUT=0 waits forever
+  static const double t = [] {
+    const char* e = std::getenv("SPFFT_COMM_TIMEOUT");
+    return e && *e ? std::max(0.0, std::atof(e)) : 120.0;
+  }();
+  return t;
 }
 
-class RcclDeviceComm : public DeviceComm {
-public:
-  // Collective on comm. Never throws between the collectives, so every rank
-  // takes part in both allgathers; ok() tells whether this rank's RCCL
-  // communicator came up (DeviceComm::create agrees on the outcome).
-  RcclDeviceComm(const std::shared_ptr<Communicator>& comm, int device, bool faultInit)
-      : comm_(comm), rank_(comm->rank()), size_(comm->size()) {
+namespace {
+
+// ------------------------------------------------------------- RCCL channel
+// One RCCL communicator plus the stream that carries every exchange issued on
+// it. Grids of one process whose communicators have the same members on the
+// same devices share one channel (DeviceComm::create): `bench.py --gpus 8`
+// with 4 transforms builds one RCCL communicator per rank, not four, and every
+// exchange of the process runs on one stream in host call order, the order
+// every rank issues them in (transforms are collective). Concurrent kernels of
+// several communicators, whose relative order can differ between ranks, are
+// the classic multi-communicator hang; a single ordered channel cannot do it.
+struct NcclChannel {
+  ncclComm_t comm = nullptr;
+  int device = 0, rank = 0, size = 0;
+  std::unique_ptr<GpuStream> stream;
+  std::unique_ptr<GpuEvent> in, out;
+  std::mutex m;
+  bool aborted = false;
+  std::string detail;  // why initialisation failed (comm == nullptr)
+
+  ~NcclChannel() {
+    if (comm && !process_exiting()) (void)ncclCommDestroy(comm);
+  }
+  bool ok() const { return comm != nullptr; }
+
+  // Non-blocking communicator calls return ncclInProgress while RCCL works in
+  // the background: poll until done, abort past the deadline (a rank that
+  // never arrives cannot leave the others inside RCCL).
+  ncclResult_t settle(ncclResult_t r, double seconds) {
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
+    while (r == ncclInProgress) {
+      if (seconds > 0 && std::chrono::duration<double>(clock::now() - t0).count() > seconds) {
+        detail = "RCCL: no progress within SPFFT_COMM_TIMEOUT = " + std::to_string(seconds) + " s";
+        return ncclInProgress;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+      if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclSystemError;
+    }
+    return r;
+  }
+
+  // Collective over `group` (rank r of the channel = rank r of group, or a
+  // size-1 channel when selfOnly). Never throws between the collectives.
+  void init(Communicator* group, bool selfOnly, int injectFault) {
     DeviceGuard guard(device);
     struct IdMsg {
       ncclUniqueId id;
@@ -45,84 +89,222 @@ public:
     IdMsg mine;
     std::memset(&mine, 0, sizeof(mine));
     mine.ok = 1;
-    if (rank_ == 0 && ncclGetUniqueId(&mine.id) != ncclSuccess) mine.ok = 0;
-    std::vector<IdMsg> all(size_);
-    comm_->allgather(&mine, all.data(), sizeof(IdMsg));
-    if (!all[0].ok) {
-      detail_ = "RCCL: ncclGetUniqueId failed on rank 0";
+    if ((selfOnly || rank == 0) && ncclGetUniqueId(&mine.id) != ncclSuccess) mine.ok = 0;
+    IdMsg root = mine;
+    if (!selfOnly) {
+      std::vector<IdMsg> all(size);
+      group->allgather(&mine, all.data(), sizeof(IdMsg));
+      root = all[0];
+    }
+    if (!root.ok) {
+      detail = "RCCL: ncclGetUniqueId failed on rank 0";
       return;
     }
-    if (faultInit) {  // fault injection (SPFFT_FAULT_RCCL_INIT=1 on every rank)
-      detail_ = "RCCL: initialisation failure injected (SPFFT_FAULT_RCCL_INIT)";
+    // fault injection: 1 = every rank fails, 2 = only the last rank fails (the
+    // others then wait for it until the init deadline and abort)
+    if (injectFault == 1 || (injectFault == 2 && rank == size - 1)) {
+      detail = "RCCL: initialisation failure injected (SPFFT_FAULT_RCCL_INIT)";
       return;
     }
-    const ncclResult_t r = ncclCommInitRank(&nccl_, size_, all[0].id, rank_);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, size, root.id, rank, &cfg);
+    if (r == ncclInProgress || r == ncclSuccess) r = settle(r, comm_timeout_seconds());
     if (r != ncclSuccess) {
-      detail_ = std::string("RCCL: ncclCommInitRank: ") + ncclGetErrorString(r);
-      nccl_ = nullptr;
+      if (detail.empty()) detail = std::string("RCCL: ncclCommInitRankConfig: ") + ncclGetErrorString(r);
+      if (comm) (void)ncclCommAbort(comm);
+      comm = nullptr;
+      return;
+    }
+    stream.reset(new GpuStream(true));
+    in.reset(new GpuEvent());
+    out.reset(new GpuEvent());
+  }
+
+  void check_usable() {
+    if (aborted || !comm) {
+      set_error_detail("RCCL: the communicator was aborted after an earlier failure");
+      throw MPIError();
     }
   }
-  bool ok() const { return nccl_ != nullptr; }
-  const std::string& detail() const { return detail_; }
-  ~RcclDeviceComm() override {
-    if (nccl_ && !process_exiting()) (void)ncclCommDestroy(nccl_);
+  void nccl_check(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) r = settle(r, comm_timeout_seconds());
+    if (r != ncclSuccess) {
+      set_error_detail(std::string("RCCL ") + what + ": " + ncclGetErrorString(r) + " " +
+                       (detail.empty() ? ncclGetLastError(comm) : detail));
+      throw MPIError();
+    }
   }
+
+  struct Xfer {
+    const char* send;  // peer-bound block (or nullptr)
+    char* recv;        // arriving block (or nullptr)
+    std::size_t bytes;
+    int peer;
+  };
+  // Enqueues the transfers after the work queued so far on `caller`; `caller`
+  // continues once every block has arrived.
+  void run(const std::vector<Xfer>& xs, hipStream_t caller) {
+    std::lock_guard<std::mutex> lock(m);
+    check_usable();
+    DeviceGuard guard(device);
+    hipStream_t cs = stream->get();
+    in->record(caller);
+    in->wait_on(cs);
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (const Xfer& x : xs) {
+      if (x.send) nccl_check(ncclSend(x.send, x.bytes, ncclChar, x.peer, comm, cs), "ncclSend");
+      if (x.recv) nccl_check(ncclRecv(x.recv, x.bytes, ncclChar, x.peer, comm, cs), "ncclRecv");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    out->record(cs);
+    out->wait_on(caller);
+  }
+
+  bool healthy(std::string* why) {
+    if (aborted) {
+      if (why) *why = "RCCL: communicator aborted";
+      return false;
+    }
+    ncclResult_t r = ncclSuccess;
+    if (!comm || ncclCommGetAsyncError(comm, &r) != ncclSuccess) return true;  // cannot tell
+    if (r == ncclSuccess || r == ncclInProgress) return true;
+    if (why) *why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
+    return false;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lock(m);
+    if (aborted || !comm) return;
+    aborted = true;
+    (void)ncclCommAbort(comm);
+    comm = nullptr;
+  }
+};
+
+// Process-wide channel registry, keyed by the member list (host, pid, device of
+// every rank, in rank order) and the device.
+std::mutex gChannelMutex;
+std::map<std::string, std::weak_ptr<NcclChannel>>& channel_registry() {
+  static auto* r = new std::map<std::string, std::weak_ptr<NcclChannel>>();  // outlives atexit
+  return *r;
+}
+std::atomic<int> gChannelsCreated{0};
+
+// SPFFT_FAULT_EXCHANGE_ABORT=N (fault injection, failure-detection tests): the
+// N-th exchange of a data plane aborts its RCCL communicator first, so that
+// exchange and every later one fail with MPIError
+int fault_abort_at() {
+  const char* e = std::getenv("SPFFT_FAULT_EXCHANGE_ABORT");
+  return e && *e ? std::atoi(e) : 0;
+}
+
+class RcclDeviceComm : public DeviceComm {
+public:
+  explicit RcclDeviceComm(std::shared_ptr<NcclChannel> ch) : ch_(std::move(ch)), faultAt_(fault_abort_at()) {}
 
   void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
                  const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
     SPFFT_TIMED_SCOPE("rccl_alltoallv");
-    if (aborted_) {
-      set_error_detail("RCCL: the communicator was aborted after an earlier failure");
-      throw MPIError();
-    }
+    if (++calls_ == faultAt_) ch_->abort();
+    ch_->check_usable();
+    const int me = ch_->rank, P = ch_->size;
     const char* s = static_cast<const char*>(send);
     char* r = static_cast<char*>(recv);
     // the local block never leaves the GPU
-    if (sc[rank_] > 0)
-      gpu_check(hipMemcpyAsync(r + rd[rank_], s + sd[rank_], static_cast<std::size_t>(sc[rank_]),
+    if (sc[me] > 0)
+      gpu_check(hipMemcpyAsync(r + rd[me], s + sd[me], static_cast<std::size_t>(sc[me]),
                                hipMemcpyDeviceToDevice, stream),
                 "hipMemcpyAsync");
-    nccl_check(ncclGroupStart());
-    for (int k = 1; k < size_; ++k) {
+    std::vector<NcclChannel::Xfer> xs;
+    xs.reserve(2 * P);
+    for (int k = 1; k < P; ++k) {
       // staggered peer order so every xGMI link is busy from the start
-      const int to = (rank_ + k) % size_;
-      const int from = (rank_ - k + size_) % size_;
-      if (sc[to] > 0) nccl_check(ncclSend(s + sd[to], static_cast<std::size_t>(sc[to]), ncclChar, to, nccl_, stream));
-      if (rc[from] > 0)
-        nccl_check(ncclRecv(r + rd[from], static_cast<std::size_t>(rc[from]), ncclChar, from, nccl_, stream));
+      const int to = (me + k) % P;
+      const int from = (me - k + P) % P;
+      if (sc[to] > 0) xs.push_back({s + sd[to], nullptr, static_cast<std::size_t>(sc[to]), to});
+      if (rc[from] > 0) xs.push_back({nullptr, r + rd[from], static_cast<std::size_t>(rc[from]), from});
     }
-    nccl_check(ncclGroupEnd());
+    if (!xs.empty()) ch_->run(xs, stream);
   }
   bool host_synchronous() const override { return false; }
   const char* kind() const override { return "rccl"; }
-  bool healthy(std::string* detail) override {
-    if (aborted_) return false;
-    ncclResult_t r = ncclSuccess;
-    if (ncclCommGetAsyncError(nccl_, &r) != ncclSuccess) return true;  // cannot tell
-    if (r == ncclSuccess || r == ncclInProgress) return true;
-    if (detail) *detail = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
-    return false;
-  }
+  bool healthy(std::string* detail) override { return ch_->healthy(detail); }
   void check() override {
     std::string d;
     if (!healthy(&d)) {
-      set_error_detail(d.empty() ? "RCCL: communicator aborted" : d);
+      set_error_detail(d);
       throw MPIError();
     }
   }
-  void abort() override {
-    if (aborted_ || !nccl_) return;
-    aborted_ = true;
-    (void)ncclCommAbort(nccl_);
-    nccl_ = nullptr;
+  void abort() override { ch_->abort(); }
+  std::string describe() const override {
+    char b[96];
+    std::snprintf(b, sizeof(b), "rccl comm %p (%d ranks, %d channels in process)",
+                  static_cast<void*>(ch_->comm), ch_->size, gChannelsCreated.load());
+    return b;
   }
 
 private:
+  std::shared_ptr<NcclChannel> ch_;
+  int faultAt_ = 0, calls_ = 0;
+};
+
+// In-process virtual ranks (local group) with every block moved by RCCL: each
+// virtual rank owns a size-1 RCCL communicator and receives the blocks of every
+// rank q (itself included) by a grouped ncclSend/ncclRecv pair to itself, on
+// the channel stream, with the real counts and displacements. This runs the
+// RCCL data path (group semantics, stream hand-off, byte layouts, async-error
+// polling, abort) on a single GPU, where RCCL refuses two ranks per device.
+class RcclSelfDeviceComm : public DeviceComm {
+public:
+  RcclSelfDeviceComm(const std::shared_ptr<Communicator>& comm, std::shared_ptr<NcclChannel> ch)
+      : comm_(comm), ch_(std::move(ch)), faultAt_(fault_abort_at()) {}
+
+  void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
+                 const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
+    SPFFT_TIMED_SCOPE("rccl_self_alltoallv");
+    if (++calls_ == faultAt_) ch_->abort();
+    ch_->check_usable();
+    const int P = comm_->size(), me = comm_->rank();
+    // every virtual rank's send buffer is complete before anyone pulls from it
+    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    struct View {
+      const char* send;
+      const std::int64_t* counts;
+      const std::int64_t* displs;
+    };
+    View mine{static_cast<const char*>(send), sc, sd};
+    std::vector<View> all(P);
+    comm_->allgather(&mine, all.data(), sizeof(View));
+    std::vector<NcclChannel::Xfer> xs;
+    for (int k = 0; k < P; ++k) {
+      const int q = (me - k + P) % P;
+      const std::int64_t n = all[q].counts[me];
+      if (n != rc[q]) throw MPIError();
+      if (n <= 0) continue;
+      xs.push_back({all[q].send + all[q].displs[me], nullptr, static_cast<std::size_t>(n), 0});
+      xs.push_back({nullptr, static_cast<char*>(recv) + rd[q], static_cast<std::size_t>(n), 0});
+    }
+    if (!xs.empty()) ch_->run(xs, stream);
+    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    comm_->barrier();  // senders may reuse their buffers only after every pull
+  }
+  bool host_synchronous() const override { return true; }
+  const char* kind() const override { return "rccl-self"; }
+  bool healthy(std::string* detail) override { return ch_->healthy(detail); }
+  void check() override {
+    std::string d;
+    if (!healthy(&d)) {
+      set_error_detail(d);
+      throw MPIError();
+    }
+  }
+  void abort() override { ch_->abort(); }
+
+private:
   std::shared_ptr<Communicator> comm_;
-  int rank_, size_;
-  ncclComm_t nccl_ = nullptr;
-  bool aborted_ = false;
-  std::string detail_;
+  std::shared_ptr<NcclChannel> ch_;
+  int faultAt_ = 0, calls_ = 0;
 };
 
 class LoopbackDeviceComm : public DeviceComm {
@@ -324,8 +506,10 @@ private:
 
 struct NodeInfo {
   std::uint64_t host;
-  int domain, bus, device;
+  long long pid;
+  int domain, bus, device, ordinal;
   int prefer;  // SPFFT_GPU_EXCHANGE: 0 auto, 1 rccl, 2 peer (ipc)
+  int fault;   // SPFFT_FAULT_RCCL_INIT (rank 0's value is used everywhere)
 };
 
 std::uint64_t host_hash() {
@@ -336,59 +520,129 @@ std::uint64_t host_hash() {
   return h;
 }
 
+int env_choice(const char* name) {
+  const char* env = std::getenv(name);
+  const std::string v = env ? env : "";
+  return v == "rccl" ? 1 : (v == "ipc" || v == "peer" ? 2 : 0);
+}
+
+int env_fault() {
+  const char* e = std::getenv("SPFFT_FAULT_RCCL_INIT");
+  return e && *e ? std::atoi(e) : 0;
+}
+
+bool share_channels() {
+  const char* e = std::getenv("SPFFT_RCCL_SHARE");
+  return !(e && *e == '0');
+}
+
+// The process's channel for `key`, created collectively if any rank lacks a
+// live one (the reuse decision is allgathered, so every rank either reuses or
+// takes part in the new communicator's initialisation).
+std::shared_ptr<NcclChannel> acquire_channel(Communicator* group, const std::string& key, int device,
+                                             int rank, int size, bool selfOnly, int fault) {
+  std::shared_ptr<NcclChannel> ch;
+  const bool share = share_channels() && fault == 0;
+  if (share) {
+    std::lock_guard<std::mutex> lock(gChannelMutex);
+    auto it = channel_registry().find(key);
+    if (it != channel_registry().end()) ch = it->second.lock();
+    if (ch && (ch->aborted || !ch->ok())) ch.reset();
+  }
+  int have = ch ? 1 : 0;
+  if (!selfOnly) {
+    std::vector<int> all(size);
+    group->allgather(&have, all.data(), sizeof(int));
+    for (int v : all) have = have && v;
+  }
+  if (have) return ch;
+  ch = std::make_shared<NcclChannel>();
+  ch->device = device;
+  ch->rank = selfOnly ? 0 : rank;
+  ch->size = selfOnly ? 1 : size;
+  ch->init(group, selfOnly, fault);
+  if (ch->ok()) {
+    ++gChannelsCreated;
+    if (share) {
+      std::lock_guard<std::mutex> lock(gChannelMutex);
+      channel_registry()[key] = ch;
+    }
+  }
+  return ch;
+}
+
 }  // namespace
+
+int DeviceComm::rccl_channels_created() { return gChannelsCreated.load(); }
 
 std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicator>& comm,
                                                int device, SpfftExchangeType exchange,
                                                void* const buffers[2]) {
   if (!comm) throw InternalError();
   const bool unbuffered = exchange == SPFFT_EXCH_UNBUFFERED;
+  const int prefLocal = env_choice("SPFFT_GPU_EXCHANGE");
   if (comm->is_local_group()) {
+    // virtual ranks of one process: SPFFT_GPU_EXCHANGE=rccl moves every block
+    // through RCCL (size-1 communicator per virtual rank); otherwise peer
+    // writes (UNBUFFERED) or device-to-device copies
+    if (prefLocal == 1) {
+      char key[64];
+      std::snprintf(key, sizeof(key), "self/%d/%d/%d", device, comm->rank(), comm->size());
+      auto ch = acquire_channel(comm.get(), key, device, comm->rank(), comm->size(), true, 0);
+      if (!ch->ok()) {
+        set_error_detail(ch->detail);
+        throw MPIError();
+      }
+      return std::unique_ptr<DeviceComm>(new RcclSelfDeviceComm(comm, ch));
+    }
     if (unbuffered) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, false));
     return std::unique_ptr<DeviceComm>(new LoopbackDeviceComm(comm));
   }
   // data-plane choice, identical on every rank (decided from allgathered facts)
   NodeInfo mine{};
   mine.host = host_hash();
-  mine.device = device;
+  mine.pid = static_cast<long long>(getpid());
+  mine.ordinal = device;
   {
     DeviceGuard guard(device);
     (void)hipDeviceGetAttribute(&mine.domain, hipDeviceAttributePciDomainID, device);
     (void)hipDeviceGetAttribute(&mine.bus, hipDeviceAttributePciBusId, device);
     (void)hipDeviceGetAttribute(&mine.device, hipDeviceAttributePciDeviceId, device);
   }
-  const char* env = std::getenv("SPFFT_GPU_EXCHANGE");
-  const std::string pref = env ? env : "";
-  mine.prefer = pref == "rccl" ? 1 : (pref == "ipc" || pref == "peer" ? 2 : 0);
+  mine.prefer = prefLocal;
+  mine.fault = env_fault();
   const int P = comm->size();
   std::vector<NodeInfo> all(P);
   comm->allgather(&mine, all.data(), sizeof(NodeInfo));
   bool oneNode = true, sharedDevice = false;
+  std::string key = "rccl";
   for (int q = 0; q < P; ++q) {
     oneNode = oneNode && all[q].host == all[0].host;
     for (int r = 0; r < q; ++r)
       sharedDevice = sharedDevice || (all[q].host == all[r].host && all[q].domain == all[r].domain &&
                                       all[q].bus == all[r].bus && all[q].device == all[r].device);
+    char m[96];
+    std::snprintf(m, sizeof(m), "/%llx:%lld:%d.%d.%d", static_cast<unsigned long long>(all[q].host),
+                  all[q].pid, all[q].domain, all[q].bus, all[q].ordinal);
+    key += m;
   }
+  // every rank decides from rank 0's settings (environments may differ)
   const int prefer = all[0].prefer;
-  // fault injection for the fallback below: every rank's RCCL initialisation
-  // reports failure (ranks sharing a device then try RCCL first as well)
-  const char* fenv = std::getenv("SPFFT_FAULT_RCCL_INIT");
-  const bool faultInit = fenv && std::atoi(fenv) != 0;
+  const int fault = all[0].fault;
   const bool peer =
-      oneNode && prefer != 1 && (unbuffered || (sharedDevice && !faultInit) || prefer == 2);
+      oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
   if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, true));
-  std::unique_ptr<RcclDeviceComm> rccl(new RcclDeviceComm(comm, device, faultInit));
+  auto ch = acquire_channel(comm.get(), key, device, comm->rank(), P, false, fault);
   // every rank learns whether every RCCL communicator came up
-  int ok = rccl->ok() ? 1 : 0;
+  int ok = ch->ok() ? 1 : 0;
   std::vector<int> oks(P);
   comm->allgather(&ok, oks.data(), sizeof(int));
   bool allOk = true;
   for (int v : oks) allOk = allOk && v != 0;
-  if (allOk) return std::unique_ptr<DeviceComm>(rccl.release());
-  const std::string why = rccl->ok() ? std::string("RCCL: another rank failed to initialise") : rccl->detail();
-  rccl->abort();
-  rccl.reset();
+  if (allOk) return std::unique_ptr<DeviceComm>(new RcclDeviceComm(ch));
+  const std::string why = ch->ok() ? std::string("RCCL: another rank failed to initialise") : ch->detail;
+  ch->abort();
+  ch.reset();
   // one node: the peer-write data plane (IPC handles over xGMI) moves the data
   // instead; across nodes there is no fallback
   if (!oneNode || prefer == 1) {

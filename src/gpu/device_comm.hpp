@@ -1,8 +1,13 @@
 // GPU data plane for the pencil <-> slab redistribution.
-//  - RcclDeviceComm: RCCL grouped send/recv (all-to-all-v) enqueued on the
-//    execution stream; xGMI peer links carry every peer pair concurrently.
-//    Replaces MPI_Alltoall(v) on staged host buffers
+//  - RcclDeviceComm: RCCL grouped send/recv (all-to-all-v) on the process's
+//    shared RCCL channel (one communicator and one ordered comm stream per
+//    member set and device, handed off to and from the caller's stream by
+//    events); xGMI peer links carry every peer pair concurrently. Replaces
+//    MPI_Alltoall(v) on staged host buffers
 //    (reference: src/transpose/transpose_mpi_compact_buffered_gpu.cpp:195-282).
+//  - RcclSelfDeviceComm: in-process virtual ranks whose blocks all move through
+//    RCCL (ncclSend/ncclRecv to self on a size-1 communicator per virtual rank):
+//    the RCCL data path on a single GPU (SPFFT_GPU_EXCHANGE=rccl).
 //  - PeerDeviceComm: zero-copy peer writes. Every rank maps the exchange
 //    buffers of every other rank (IPC handles across processes, plain pointers
 //    inside a local group); the producing stage kernel (z-stage backward,
@@ -26,6 +31,11 @@
 #include "spfft/types.h"
 
 namespace spfft {
+
+// Seconds a distributed call may wait for its data plane (RCCL initialisation,
+// the watched stream wait) before it aborts the data plane and throws
+// MPIError. SPFFT_COMM_TIMEOUT, default 120; 0 = no limit.
+double comm_timeout_seconds();
 
 class DeviceComm {
 public:
@@ -70,6 +80,10 @@ public:
   // data plane is unusable afterwards: every later exchange throws MPIError.
   virtual void abort() {}
   virtual const char* kind() const = 0;
+  // One line for SPFFT_LOG (e.g. which RCCL communicator a grid uses).
+  virtual std::string describe() const { return kind(); }
+  // RCCL communicators this process has created (shared channels count once).
+  static int rccl_channels_created();
 };
 
 }  // namespace spfft

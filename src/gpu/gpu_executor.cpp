@@ -150,7 +150,7 @@ void GpuExecutor<T>::log_plan() const {
   const IndexPlan& p = *plan_;
   const bool dbl = sizeof(T) == 8;
   std::string plane = "none";
-  if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().kind();
+  if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
                "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d peer_writes=%d fused=%d\n",
@@ -544,17 +544,14 @@ void GpuExecutor<T>::harvest_stage_times(bool wait) {
 // Failure detection for distributed transforms: the
 // host polls the stream and, every millisecond, the data plane's asynchronous
 // error state (RCCL: ncclCommGetAsyncError; peer writes: barrier timeouts). A
-// failure, or a wait longer than SPFFT_COMM_TIMEOUT seconds (0 = no limit, the
-// default), aborts the data plane (ncclCommAbort / barrier kernels released)
+// failure, or a wait longer than SPFFT_COMM_TIMEOUT seconds (default 120,
+// 0 = no limit), aborts the data plane (ncclCommAbort / barrier kernels released)
 // and throws MPIError with the cause in the error detail, instead of leaving
 // the caller blocked forever on a dead peer.
 template <typename T>
 void GpuExecutor<T>::wait_stream_watched() {
   DeviceComm& dc = grid_->device_comm();
-  static const double timeout = [] {
-    const char* e = std::getenv("SPFFT_COMM_TIMEOUT");
-    return e && *e ? std::max(0.0, std::atof(e)) : 0.0;
-  }();
+  const double timeout = comm_timeout_seconds();
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   auto last = t0;

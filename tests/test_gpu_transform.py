@@ -814,3 +814,128 @@ def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, monkeypatch):
 
     for e in run_ranks(P, body):
         assert e < 1e-11
+
+
+# ------------------------------------------------------------ RCCL data plane
+# SPFFT_GPU_EXCHANGE=rccl on an in-process group: every exchange block of every
+# virtual rank moves through RCCL (grouped ncclSend/ncclRecv to self on a size-1
+# communicator per virtual rank, on the shared channel stream, with the real
+# counts and displacements). RCCL refuses two ranks of one communicator on one
+# device (profiles/r3/rccl_duplicate_device.txt), so this is how the RCCL data
+# path runs on the one-GPU box.
+@pytest.mark.parametrize("exchange,chunks", [("COMPACT_BUFFERED", 1), ("COMPACT_BUFFERED", 2),
+                                             ("COMPACT_BUFFERED", 4), ("COMPACT_BUFFERED_FLOAT", 1),
+                                             ("COMPACT_BUFFERED_FLOAT", 3), ("BUFFERED", 1),
+                                             ("BUFFERED", 2), ("BUFFERED_FLOAT", 1),
+                                             ("UNBUFFERED", 1), ("UNBUFFERED", 2)])
+@pytest.mark.parametrize("P", [3, 8])
+def test_gpu_virtual_ranks_rccl(gpu, P, exchange, chunks, monkeypatch):
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    dims = (24, 20, 18) if P == 3 else (32, 28, 40)
+    gidx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(31 + P)
+    vals = _rand_vals(rng, len(gidx))
+    ref = dense_backward(gidx, vals, dims)
+    parts = distribute_sticks(gidx, P, dims)
+    tol = 1e-6 if exchange.endswith("FLOAT") else 1e-12
+    ex = getattr(sp.ExchangeType, exchange)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU, exchange_type=ex)
+        plane = s.grid.data_plane
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.as_tensor(vals[start:start + len(s.indices)], device="cuda")
+        errs = []
+        for _ in range(2):  # run twice: stale or missing blocks show up
+            out = s.transform.backward(v).cpu().numpy()
+            errs.append(max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length]))
+            f = s.transform.forward(None, scaling=sp.Scaling.FULL).cpu().numpy()
+            errs.append(max_rel_error(f, v.cpu().numpy()))
+        return plane, max(errs)
+
+    for plane, e in run_ranks(P, body):
+        assert plane == "rccl-self"
+        assert e < tol
+
+
+def test_rccl_channel_shared_across_grids(gpu, monkeypatch):
+    """Grids of one rank share one RCCL communicator: 3 grids per virtual rank
+    (multi_transform of 3 transforms) create one communicator per rank, not 3."""
+    import torch
+    from spfft_amd.parallel import run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
+    dims = (20, 16, 12)
+    nx, ny, nz = dims
+    P = 2
+    gidx = sphere_indices(*dims, 0.5)
+    parts = distribute_sticks(gidx, P, dims)
+    planes = [nz // P] * P
+    rng = np.random.default_rng(5)
+    vals = [_rand_vals(rng, len(gidx)) for _ in range(3)]
+    refs = [dense_backward(gidx, v, dims) for v in vals]
+    starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
+    max_sticks = max(len(np.unique(p[:, 0] * ny + p[:, 1])) for p in parts)
+    import gc
+    gc.collect()  # grids of earlier tests release their channels
+    before = sp.rccl_communicators()
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        ts = []
+        for _ in range(3):
+            g = sp.Grid(nx, ny, nz, max_sticks, GPU, 1, max_local_z_length=max(planes), comm=comm,
+                        exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+            ts.append(g.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
+                                         parts[rank]))
+        ins = [torch.as_tensor(v[starts[rank]:starts[rank + 1]], device="cuda") for v in vals]
+        outs = sp.multi_transform_backward(ts, ins)
+        z0 = rank * planes[0]
+        e = max(max_rel_error(o.cpu().numpy(), r[z0:z0 + planes[rank]]) for o, r in zip(outs, refs))
+        back = sp.multi_transform_forward(ts, scalings=[sp.Scaling.FULL] * 3)
+        e2 = max(max_rel_error(b.cpu().numpy(), i.cpu().numpy()) for b, i in zip(back, ins))
+        return max(e, e2)
+
+    for e in run_ranks(P, body):
+        assert e < 1e-12
+    # one per virtual rank (fewer if an earlier test's channel is still alive), not 3P
+    assert 0 <= sp.rccl_communicators() - before <= P
+
+
+def test_rccl_abort_is_reported(gpu, monkeypatch):
+    """Failure detection on the RCCL plane: the 2nd exchange aborts the communicator
+    (ncclCommAbort on a live RCCL communicator, SPFFT_FAULT_EXCHANGE_ABORT=2); that
+    call and every later exchange raise MPIError instead of hanging."""
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
+    monkeypatch.setenv("SPFFT_RCCL_SHARE", "0")
+    monkeypatch.setenv("SPFFT_FAULT_EXCHANGE_ABORT", "2")
+    dims = (16, 12, 10)
+    gidx = sphere_indices(*dims, 0.5)
+    from spfft_amd.utils.indices import distribute_sticks
+    parts = distribute_sticks(gidx, 2, dims)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU)
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.ones(len(s.indices), dtype=torch.complex128, device="cuda")
+        s.transform.backward(v)  # exchange 1: fine
+        msgs = []
+        for _ in range(2):
+            try:
+                s.transform.forward(None)
+                msgs.append(None)
+            except sp.MPIError as err:
+                msgs.append(str(err))
+        del start
+        return msgs
+
+    for msgs in run_ranks(2, body):
+        assert all(m is not None and "abort" in m for m in msgs), msgs

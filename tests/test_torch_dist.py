@@ -2,8 +2,12 @@
 plane, one OS process per rank), the same launch path bench.py uses.
 
 CPU: host transforms, every exchange type, 2 and 3 ranks.
-GPU: 2 ranks sharing the box's single MI355X — exercises the library's RCCL
-communicator bootstrap (ncclUniqueId via allgather) and grouped send/recv.
+GPU: 2-3 ranks sharing the box's single MI355X. RCCL refuses two ranks of one
+communicator on one device (profiles/r3/rccl_duplicate_device.txt), so these
+runs move data with the IPC peer-write plane; the RCCL initialisation-failure
+agreement and fallback are covered by fault injection. The RCCL send/recv data
+path itself runs in tests/test_gpu_transform.py (test_gpu_virtual_ranks_rccl,
+RCCL self-loopback per virtual rank).
 """
 import os
 import socket
