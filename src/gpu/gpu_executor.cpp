@@ -46,11 +46,6 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
                                  env_int("SPFFT_PAD_STICK", 8, 0, kMaxPad));
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
-  chunkPlanes_ = env_int("SPFFT_CHUNK_PLANES", 0, 0, 1 << 20);
-  // [z][column][y] (plane-major, default) or [column][z][y] intermediate
-  interLayout_ = env_int("SPFFT_INTER_LAYOUT", 0, 0, 2);
-  if (interLayout_ == 2 && p.num_columns() % 8 != 0) interLayout_ = 0;  // whole blocks only
-  interRing_ = chunkPlanes_ > 0 && interLayout_ == 0 && env_int("SPFFT_INTER_RING", 0, 0, 1) != 0;
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
   // launches in stream-ordered use (profiles/README.md, session 6)
@@ -96,11 +91,9 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(twY_, make_twiddles<T>(p.dimY));
   upload(twZ_, make_twiddles<T>(p.dimZ));
 
-  if (!distributed) setup_fused();
   batchEnabled_ = env_int("SPFFT_BATCH", 1, 0, 1) != 0;
   batchLarge_ = env_int("SPFFT_BATCH_LARGE", 1 << 22, 0, std::numeric_limits<int>::max());
   batchSplit_ = env_int("SPFFT_BATCH_SPLIT", 2, 1, dev::kMaxBatch);
-  xySplit_ = env_int("SPFFT_XY_SPLIT", 0, 0, 1) != 0;
   compute_batch_key();
 
   if (distributed) {
@@ -136,13 +129,13 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     std::vector<int> all(p.size);
     grid_->communicator()->allgather(&chunks, all.data(), sizeof(int));
     chunks = all[0];
-    if (!peerWrites_ && chunkPlanes_ == 0 && chunks > 1) build_chunk_plan(chunks);
+    if (!peerWrites_ && chunks > 1) build_chunk_plan(chunks);
   }
   log_plan();
 }
 
 // SPFFT_LOG=1: one line per transform with the plan decisions (engines, layout,
-// data plane, pipelining, fused path)
+// data plane, pipelining)
 template <typename T>
 void GpuExecutor<T>::log_plan() const {
   const char* env = std::getenv("SPFFT_LOG");
@@ -153,7 +146,7 @@ void GpuExecutor<T>::log_plan() const {
   if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
-               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d peer_writes=%d fused=%d\n",
+               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d peer_writes=%d\n",
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
@@ -161,8 +154,7 @@ void GpuExecutor<T>::log_plan() const {
                dev::describe_engine(p.dimY, dbl, true).c_str(),
                dev::describe_engine(twXh_ ? p.dimX / 2 : p.dimX, dbl, true).c_str(),
                twXh_ ? " packed-real" : "", layout_.buffered ? "buffered" : "compact",
-               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, peerWrites_ ? 1 : 0,
-               fused_ ? 1 : 0);
+               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, peerWrites_ ? 1 : 0);
 }
 
 template <typename T>
@@ -370,81 +362,8 @@ GpuExecutor<T>::~GpuExecutor() {
     DeviceGuard guard(deviceId_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.exec);
-    if (fusedFailHost_) (void)hipHostFree(fusedFailHost_);
   } catch (...) {
   }
-}
-
-template <typename T>
-void GpuExecutor<T>::setup_fused() {
-  const IndexPlan& p = *plan_;
-  if (p.size != 1 || p.type != SPFFT_TRANS_C2C || !p.simpleSticks || chunkPlanes_ != 0) return;
-  // opt-in (SPFFT_FUSED=1): measured slower than the three-kernel path on MI355X
-  // (profiles/README.md, "fused y/x experiment")
-  if (!env_int("SPFFT_FUSED", 0, 0, 1) || !dev::fused_supported(p.dimX, p.dimY, p.dimZ)) return;
-  const int S = p.local_sticks(), ncols = p.num_columns();
-  if (S < 1 || ncols < 1) return;
-  for (std::size_t e = 0; e < p.colLocal.size(); ++e)
-    if (p.colLocal[e] != static_cast<int>(e)) return;  // entries must be the stick order
-  const long long Sp = S + env_int("SPFFT_PAD_STICK", 8, 0, kMaxPad);
-  if (static_cast<long long>(p.dimZ) * Sp > grid_->slot_elements(GridImpl<T>::kStickSide)) return;
-  int cus = 0;
-  gpu_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, deviceId_),
-            "hipDeviceGetAttribute");
-  const int bpc = std::min(2, dev::fused_blocks_per_cu<T>(p.dimX, p.dimY));
-  if (cus < 1 || bpc < 1) return;
-  std::vector<int> entryCol(p.colY.size());
-  for (int c = 0; c < ncols; ++c)
-    for (int e = p.colOffsets[c]; e < p.colOffsets[c + 1]; ++e) entryCol[e] = c;
-  upload(entryCol_, entryCol);
-  const int lag = env_int("SPFFT_FUSED_LAG", 2, 1, dev::kMaxRing - 1);
-  const int ring = std::max(lag + 1, env_int("SPFFT_FUSED_RING", lag + 2, 2, dev::kMaxRing));
-  const long long stride = ncols + 8;
-  fscratch_.reset(new DeviceBuffer(static_cast<std::size_t>(8) * ring * p.dimY * stride * sizeof(cx<T>)));
-  fctrl_.reset(new DeviceBuffer(dev::kFusedCtrlWords * sizeof(unsigned)));
-  gpu_check(hipHostMalloc(reinterpret_cast<void**>(&fusedFailHost_), 64,
-                          hipHostMallocMapped | hipHostMallocCoherent),
-            "hipHostMalloc");
-  *fusedFailHost_ = 0;
-  unsigned* failDev = nullptr;
-  gpu_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev), fusedFailHost_, 0),
-            "hipHostGetDevicePointer");
-  int rateKHz = 0;
-  gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, deviceId_),
-            "hipDeviceGetAttribute");
-  dev::FusedArgs& a = fargs_;
-  a.S = S;
-  a.Sp = Sp;
-  a.X = p.dimX;
-  a.Y = p.dimY;
-  a.Z = p.dimZ;
-  a.ncols = ncols;
-  a.colOffsets = colOffsets_->data<int>();
-  a.colY = colY_->data<int>();
-  a.colX = colX_->data<int>();
-  a.entryCol = entryCol_->data<int>();
-  a.desc = descs_->data<StickDesc>();
-  a.scratchStride = stride;
-  a.scratchPlane = static_cast<long long>(p.dimY) * stride;
-  a.ring = ring;
-  a.lag = lag;
-  a.debug = env_int("SPFFT_FUSED_DEBUG", 0, 0, 255);
-  a.ctrl = fctrl_->data<unsigned>();
-  a.failure = failDev;
-  a.timeout = static_cast<long long>(2.0 * 1e3 * std::max(rateKHz, 1));  // 2 s
-  fusedGrid_ = cus * bpc;
-  fused_ = true;
-}
-
-template <typename T>
-void GpuExecutor<T>::check_fused() {
-  if (!fusedFailHost_ || __atomic_load_n(fusedFailHost_, __ATOMIC_ACQUIRE) == 0) return;
-  // a persistent kernel could not synchronise its workgroups (grid not resident,
-  // e.g. a shared GPU): results of that call are invalid; fall back for good
-  *fusedFailHost_ = 0;
-  fused_ = false;
-  set_error_detail("fused y/x kernel: workgroup synchronisation timed out; fused path disabled");
-  throw GPUError();
 }
 
 template <typename T>
@@ -467,7 +386,6 @@ void GpuExecutor<T>::synchronize() {
   if (!traces_.empty()) harvest_stage_times(false);
   // a peer barrier that timed out leaves a flag behind (data are incomplete)
   if (peerWrites_) grid_->device_comm().check();
-  check_fused();
 }
 
 template <typename T>
@@ -583,7 +501,7 @@ template <typename T>
 bool GpuExecutor<T>::graph_eligible() const {
   // single rank only: exchanges (RCCL, peer barriers) stay outside graphs; the
   // legacy default stream cannot be captured
-  return graphsEnabled_ && plan_->size == 1 && !fused_ && !poison_ && !gpu_sync_debug() &&
+  return graphsEnabled_ && plan_->size == 1 && !poison_ && !gpu_sync_debug() &&
          stream_ != nullptr;
 }
 
@@ -722,29 +640,6 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
 }
 
 template <typename T>
-void GpuExecutor<T>::inter_strides(long long& zStride, long long& bStride, long long& cStride) const {
-  const IndexPlan& p = *plan_;
-  const long long S = interStride_;
-  const long long L = p.local_planes();
-  switch (interLayout_) {
-    case 1:  // column-major [c][z][y]
-      zStride = S;
-      cStride = L * S;
-      bStride = 8 * cStride;
-      break;
-    case 2:  // blocked [c/8][z][c%8][y]
-      zStride = 8 * S;
-      cStride = S;
-      bStride = 8 * L * S;
-      break;
-    default:  // plane-major [z][c][y]
-      zStride = static_cast<long long>(p.num_columns()) * S;
-      cStride = S;
-      bStride = 8 * S;
-  }
-}
-
-template <typename T>
 dev::YArgs GpuExecutor<T>::yargs() const {
   const IndexPlan& p = *plan_;
   dev::YArgs a{};
@@ -756,7 +651,7 @@ dev::YArgs GpuExecutor<T>::yargs() const {
   a.n = p.dimY;
   a.colOfX0 = p.type == SPFFT_TRANS_R2C ? p.colOfX0 : -1;
   a.interStride = interStride_;
-  inter_strides(a.interZStride, a.interBStride, a.interCStride);
+  a.interZStride = static_cast<long long>(p.num_columns()) * interStride_;
   a.colOffsets = colOffsets_ ? colOffsets_->data<int>() : nullptr;
   a.colY = colY_ ? colY_->data<int>() : nullptr;
   a.colBase = colBase_ ? colBase_->data<long long>() : nullptr;
@@ -775,7 +670,7 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   a.nFreq = p.dimXFreq;
   a.ncols = p.num_columns();
   a.interStride = interStride_;
-  inter_strides(a.interZStride, a.interBStride, a.interCStride);
+  a.interZStride = static_cast<long long>(p.num_columns()) * interStride_;
   a.colX = colX_ ? colX_->data<int>() : nullptr;
   return a;
 }
@@ -826,11 +721,6 @@ void GpuExecutor<T>::backward_z(const T* input) {
     }
   }
   void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
-  if (fused_) {
-    dev::launch_z_backward_pm<T>(fargs_, values, static_cast<cx<T>*>(stick), twZ_->data<cx<T>>(),
-                                 stream_);
-    return;
-  }
   auto a = zargs();
   if (peerWrites_) {
     // the z stage stores straight into the peers' slab sides
@@ -864,7 +754,8 @@ void GpuExecutor<T>::exchange(bool backward) {
 template <typename T>
 void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_backward_exchange");
-  StageEnd stageEnd{this, "backward", "exchange"};
+  // pipelined: the exchange runs on the comm stream, inside "exchange+y+x"
+  StageEnd stageEnd{this, "backward", exchChunks_ > 1 ? nullptr : "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
@@ -883,78 +774,33 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   if (outputLocation != SPFFT_PU_HOST && outputLocation != SPFFT_PU_GPU)
     throw InvalidParameterError();
   DeviceGuard guard(deviceId_);
-  StageEnd stageEnd{this, "backward", "y+x"};
+  StageEnd stageEnd{this, "backward", exchChunks_ > 1 ? "exchange+y+x" : "y+x"};
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
-  auto* interBase = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
-  if (fused_) {
-    gpu_check(hipMemsetAsync(fctrl_->data(), 0, dev::kFusedCtrlWords * sizeof(unsigned), stream_),
-              "hipMemsetAsync");
-    dev::launch_yx_backward<T>(fargs_, fusedGrid_,
-                               static_cast<const cx<T>*>(grid_->device_slot(GridImpl<T>::kStickSide)),
-                               static_cast<cx<T>*>(space), fscratch_->data<cx<T>>(),
-                               twY_->data<cx<T>>(), twX_->data<cx<T>>(), stream_);
-    if (outputLocation == SPFFT_PU_HOST) {
-      gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
-                               hipMemcpyDeviceToHost, stream_),
-                "hipMemcpyAsync");
-    }
-    return;
-  }
-  if (exchChunks_ > 1) {
-    // pipelined exchange: the y/x stages of chunk k start when it has arrived
-    for (int k = 0; k < exchChunks_; ++k) {
+  // pipelined exchange: the y/x stages of chunk k start when it has arrived
+  const int K = exchChunks_ > 1 ? exchChunks_ : 1;
+  for (int k = 0; k < K; ++k) {
+    auto ya = yargs();
+    auto xa = xargs();
+    if (K > 1) {
       chunkEvents_[k]->wait_on(stream_);
-      auto ya = yargs();
-      auto xa = xargs();
       ya.zBegin = xa.zBegin = planeBounds_[k];
       ya.L = xa.L = planeBounds_[k + 1];
       if (ya.L <= ya.zBegin) continue;
       ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
       set_col_desc(ya, colDescChunk_[k]);
-      if (floatExchange_)
-        dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), interBase,
-                                             twY_->data<cx<T>>(), stream_);
-      else
-        dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), interBase,
-                                         twY_->data<cx<T>>(), stream_);
-      dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, interBase, space,
-                                twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
-                                stream_);
     }
-    if (outputLocation == SPFFT_PU_HOST) {
-      gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
-                               hipMemcpyDeviceToHost, stream_),
-                "hipMemcpyAsync");
-    }
-    return;
-  }
-  // plane chunks: the intermediate of a chunk is read back by the x stage while
-  // it is still resident in the last-level (Infinity) cache
-  const int L = plan_->local_planes();
-  const bool split = xy_split_active();
-  const int chunk = split ? (L + 1) / 2 : (chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1));
-  if (split) xy_fork();
-  for (int zb = 0; zb < L; zb += chunk) {
-    const hipStream_t s = split && zb > 0 ? helperStream_->get() : stream_;
-    auto ya = yargs();
-    auto xa = xargs();
-    ya.zBegin = xa.zBegin = zb;
-    ya.L = xa.L = std::min(L, zb + chunk);
-    // ring mode: every chunk reuses the first `chunk` planes of the intermediate
-    cx<T>* inter =
-        interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
     if (floatExchange_)
       dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
-                                           twY_->data<cx<T>>(), s);
+                                           twY_->data<cx<T>>(), stream_);
     else
       dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
-                                       twY_->data<cx<T>>(), s);
-    dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space,
-                              twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, s);
+                                       twY_->data<cx<T>>(), stream_);
+    dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space, twX_->data<cx<T>>(),
+                              twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
   }
-  if (split) xy_join();
   if (outputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
                              hipMemcpyDeviceToHost, stream_),
@@ -979,101 +825,44 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
               "hipMemcpyAsync");
   }
   poison(false);
-  if (fused_) {
-    gpu_check(hipMemsetAsync(fctrl_->data(), 0, dev::kFusedCtrlWords * sizeof(unsigned), stream_),
-              "hipMemsetAsync");
-    dev::launch_xy_forward<T>(fargs_, fusedGrid_, static_cast<const cx<T>*>(space),
-                              static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kStickSide)),
-                              fscratch_->data<cx<T>>(), twY_->data<cx<T>>(), twX_->data<cx<T>>(),
-                              stream_);
-    return;
-  }
-  auto* interBase = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
+  auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides
   if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
-  if (exchChunks_ > 1) {
-    // pipelined exchange: chunk k's all-to-all starts when its y stage is done
-    for (int k = 0; k < exchChunks_; ++k) {
-      auto ya = yargs();
-      auto xa = xargs();
-      ya.zBegin = xa.zBegin = planeBounds_[k];
-      ya.L = xa.L = planeBounds_[k + 1];
-      if (ya.L > ya.zBegin) {
-        ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
-        set_col_desc(ya, colDescChunk_[k]);
-        dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, interBase,
-                                 twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr,
-                                 stream_);
-        if (floatExchange_)
-          dev::launch_y_forward<T, cx<float>>(ya, interBase, static_cast<cx<float>*>(slab),
-                                              twY_->data<cx<T>>(), stream_);
-        else
-          dev::launch_y_forward<T, cx<T>>(ya, interBase, static_cast<cx<T>*>(slab),
-                                          twY_->data<cx<T>>(), stream_);
-      }
-      chunkEvents_[k]->record(stream_);
-    }
-    return;
-  }
-  const int L = plan_->local_planes();
-  const bool split = xy_split_active();
-  const int chunk = split ? (L + 1) / 2 : (chunkPlanes_ > 0 ? chunkPlanes_ : std::max(L, 1));
-  if (split) xy_fork();
-  for (int zb = 0; zb < L; zb += chunk) {
-    const hipStream_t s = split && zb > 0 ? helperStream_->get() : stream_;
+  // pipelined exchange: chunk k's all-to-all starts when its y stage is done
+  const int K = exchChunks_ > 1 ? exchChunks_ : 1;
+  for (int k = 0; k < K; ++k) {
     auto ya = yargs();
     auto xa = xargs();
-    ya.zBegin = xa.zBegin = zb;
-    ya.L = xa.L = std::min(L, zb + chunk);
-    cx<T>* inter =
-        interBase - (interRing_ ? static_cast<long long>(zb) * ya.ncols * ya.interStride : 0);
-    if (peerWrites_) {
+    if (K > 1) {
+      ya.zBegin = xa.zBegin = planeBounds_[k];
+      ya.L = xa.L = planeBounds_[k + 1];
+      ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
+      set_col_desc(ya, colDescChunk_[k]);
+    } else if (peerWrites_) {
       ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
       set_col_desc(ya, colDescRemote_);
       ya.remote = 1;
     }
-    dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter,
-                             twX_->data<cx<T>>(), twXh_ ? twXh_->data<cx<T>>() : nullptr, s);
-    if (floatExchange_)
-      dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
-                                          twY_->data<cx<T>>(), s);
-    else
-      dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
-                                      s);
+    if (ya.L > ya.zBegin) {
+      dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter, twX_->data<cx<T>>(),
+                               twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+      if (floatExchange_)
+        dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+                                            twY_->data<cx<T>>(), stream_);
+      else
+        dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
+                                        stream_);
+    }
+    if (K > 1) chunkEvents_[k]->record(stream_);
   }
-  if (split) xy_join();
-}
-
-template <typename T>
-bool GpuExecutor<T>::xy_split_active() const {
-  return xySplit_ && plan_->size == 1 && !fused_ && chunkPlanes_ == 0 && !interRing_ &&
-         !capturing_ && plan_->local_planes() >= 2 && batch_large();
-}
-
-// the helper stream starts after the work queued so far on the execution stream
-template <typename T>
-void GpuExecutor<T>::xy_fork() {
-  if (!helperStream_) {
-    helperStream_.reset(new GpuStream());
-    forkEvent_.reset(new GpuEvent());
-    helperDone_.reset(new GpuEvent());
-  }
-  forkEvent_->record(stream_);
-  forkEvent_->wait_on(helperStream_->get());
-}
-
-// the execution stream continues after the helper stream's half
-template <typename T>
-void GpuExecutor<T>::xy_join() {
-  helperDone_->record(helperStream_->get());
-  helperDone_->wait_on(stream_);
 }
 
 template <typename T>
 void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_forward_exchange");
-  StageEnd stageEnd{this, "forward", "exchange"};
+  // pipelined: only the exchange's tail after the last y stage is left here
+  StageEnd stageEnd{this, "forward", exchChunks_ > 1 ? "exchange-tail" : "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
@@ -1102,16 +891,6 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   if (hostOut) values = staging(p.numLocalElements);
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kStickSide);
-  if (fused_) {
-    dev::launch_z_forward_pm<T>(fargs_, static_cast<const cx<T>*>(stick), values, factor,
-                                twZ_->data<cx<T>>(), stream_);
-    if (hostOut) {
-      gpu_check(hipMemcpyAsync(output, values, sizeof(cx<T>) * p.numLocalElements,
-                               hipMemcpyDeviceToHost, stream_),
-                "hipMemcpyAsync");
-    }
-    return;
-  }
   const auto a = zargs();
   if (floatExchange_)
     dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,
@@ -1151,7 +930,7 @@ void GpuExecutor<T>::compute_batch_key() {
   const IndexPlan& p = *plan_;
   Fnv f;
   for (int v : {static_cast<int>(p.type), p.dimX, p.dimY, p.dimZ, p.numLocalElements, p.zeroStick,
-                p.colOfX0, deviceId_, interLayout_, static_cast<int>(sizeof(T))})
+                p.colOfX0, deviceId_, static_cast<int>(sizeof(T))})
     f.value(v);
   f.value(interStride_);
   f.vec(layout_.stickStride);
@@ -1168,8 +947,8 @@ void GpuExecutor<T>::compute_batch_key() {
 
 template <typename T>
 bool GpuExecutor<T>::batchable() const {
-  return batchEnabled_ && plan_->size == 1 && !fused_ && !peerWrites_ && exchChunks_ <= 1 &&
-         chunkPlanes_ == 0 && !interRing_ && !capturing_ && !poison_;
+  return batchEnabled_ && plan_->size == 1 && !peerWrites_ && exchChunks_ <= 1 && !capturing_ &&
+         !poison_;
 }
 
 // A member needs no stream join when it runs on the leader's stream, or when

@@ -12,7 +12,6 @@
 
 #include "api/grid_impl.hpp"
 #include "gpu/gpu_runtime.hpp"
-#include "kernels/fused_stage.hpp"
 #include "kernels/stage_args.hpp"
 #include "plan/index_plan.hpp"
 
@@ -103,12 +102,6 @@ private:
   ExchangeLayout layout_;
   bool floatExchange_ = false;
   long long interStride_ = 0;  // row stride of [z][column][y]
-  int chunkPlanes_ = 0;        // y/x stages interleaved per chunk of planes (0 = off)
-  bool interRing_ = false;     // plane chunks share one chunk-sized intermediate (cache-resident)
-  // SPFFT_INTER_LAYOUT: 0 plane-major [z][column][y] (default), 1 column-major
-  // [column][z][y], 2 blocked [column/8][z][column%8][y]
-  int interLayout_ = 0;
-  void inter_strides(long long& zStride, long long& bStride, long long& cStride) const;
   bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;
 
@@ -122,16 +115,6 @@ private:
   long long batchLarge_ = 0;  // slab elements from which joins are allowed
   int batchSplit_ = 2;        // sub-batch size of large grids
   std::unique_ptr<GpuEvent> joinEvent_, doneEvent_;
-  // Single-rank y/x stages split into two plane halves on two streams (fork /
-  // join by events), so one half's y stage overlaps the other's x stage and the
-  // kernel tails fill each other (SPFFT_XY_SPLIT=1; large grids only). Measured
-  // 4-8% slower at 256^3 (profiles/r2_s3/xy_split.txt): off by default.
-  bool xySplit_ = false;
-  std::unique_ptr<GpuStream> helperStream_;
-  std::unique_ptr<GpuEvent> forkEvent_, helperDone_;
-  bool xy_split_active() const;
-  void xy_fork();
-  void xy_join();
   static void batch_join(const std::vector<GpuExecutor*>& ex);
   static void batch_release(const std::vector<GpuExecutor*>& ex);
   bool batch_needs_join(const GpuExecutor& leader) const {
@@ -172,16 +155,6 @@ private:
   long long slab_offset() const;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
 
-  // Fused single-GPU path (P = 1, C2C): plane-major sticks and the persistent
-  // XCD-cooperative y/x kernels (kernels/fused_stage.hip). Opt-in: SPFFT_FUSED=1.
-  bool fused_ = false;
-  int fusedGrid_ = 0;
-  dev::FusedArgs fargs_{};
-  std::unique_ptr<DeviceBuffer> entryCol_, fscratch_, fctrl_;
-  unsigned* fusedFailHost_ = nullptr;
-  void setup_fused();
-  void check_fused();
-
   // Pipelined exchange (RCCL / loopback data planes, compact layout): every
   // rank's planes are split into K chunks and both exchange buffers are laid
   // out chunk-major, so chunk k is one contiguous block per peer. Backward: the
@@ -220,6 +193,7 @@ private:
     const char* dir;
     const char* stage;
     ~StageEnd() {
+      if (!stage) return;  // nothing ends here
       try {
         e->stage_mark(dir, stage);
       } catch (...) {

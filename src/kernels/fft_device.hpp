@@ -28,64 +28,6 @@ namespace dev {
 
 constexpr int kMaxThreads = 256;
 
-// Paired fp32 lanes: f2 holds one float from each of two adjacent lines, so
-// cx<f2> carries two complex<float> values and every butterfly runs on packed
-// fp32 instructions (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32): half the
-// VALU instructions per element of the scalar fp32 engine, whose stage kernels
-// issue as many VALU instructions per kernel as the fp64 ones for half the
-// bytes (profiles/r2_pmc32).
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-// Element-type traits of the FFT engines: twiddle precision, and how a lane
-// element is kept in LDS. Paired elements are stored as the two complex<float>
-// values of lines 2p and 2p+1 side by side, so the stage kernels address single
-// lines of an LDS tile whichever engine filled it.
-template <typename T>
-struct LaneElem {
-  using Tw = T;
-  static constexpr bool kPair = false;
-};
-template <>
-struct LaneElem<f2> {
-  using Tw = float;
-  static constexpr bool kPair = true;
-};
-template <typename T>
-__device__ __forceinline__ cx<T> tw_elem(cx<typename LaneElem<T>::Tw> w) {
-  if constexpr (LaneElem<T>::kPair) {
-    return mk<T>(T(w.x), T(w.y));
-  } else {
-    return w;
-  }
-}
-template <typename T>
-__device__ __forceinline__ void lds_put(cx<T>* p, cx<T> v) {
-  if constexpr (LaneElem<T>::kPair) {
-    f4 q;
-    q.x = v.x.x;
-    q.y = v.y.x;
-    q.z = v.x.y;
-    q.w = v.y.y;
-    *reinterpret_cast<f4*>(p) = q;
-  } else {
-    *p = v;
-  }
-}
-template <typename T>
-__device__ __forceinline__ cx<T> lds_get(const cx<T>* p) {
-  if constexpr (LaneElem<T>::kPair) {
-    const f4 q = *reinterpret_cast<const f4*>(p);
-    f2 re, im;
-    re.x = q.x;
-    re.y = q.z;
-    im.x = q.y;
-    im.y = q.w;
-    return mk<T>(re, im);
-  } else {
-    return *p;
-  }
-}
 #ifndef SPFFT_LDS_BUDGET
 #define SPFFT_LDS_BUDGET (64 * 1024)
 #endif
@@ -115,8 +57,6 @@ struct LdsGeom<double> {
   static constexpr int kShift = 4;  // 16 x 16 B elements per 256 B bank row
   static constexpr int kMod = 16;
 };
-template <>
-struct LdsGeom<f2> : LdsGeom<double> {};  // 16-byte elements, like complex<double>
 template <>
 struct LdsGeom<float> {
   static constexpr int kShift = 5;  // 32 x 8 B elements per bank row
@@ -232,9 +172,6 @@ struct CtShape256E8 {
 };
 template <typename T, int N, int S, bool LF>
 struct CtShapeSel : std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::type {};
-// a paired fp32 element has the size of a complex<double>: same shapes
-template <int N, int S, bool LF>
-struct CtShapeSel<f2, N, S, LF> : CtShapeSel<double, N, S, LF> {};
 // N = 128 likewise (radices 8, 8, 2; 16 lanes per line): 256^3 R2C 6467 ->
 // 6820 transforms/s (packed-real x stage on N/2 = 128), 128^3 C2C 23770 ->
 // 25550 (profiles/r2_s1/shape_ab.txt)
@@ -405,7 +342,7 @@ struct FftCT {
 
   // butterflies of one pass on the lane's registers (input order: v[k*R + r]
   // holds element j + r*N/R with j = t + k*TP)
-  using TwT = typename LaneElem<T>::Tw;  // twiddle table precision
+  using TwT = T;  // twiddle table precision
 
   template <int R, int NS>
   __device__ static void compute(cx<T> (&v)[E], int t, const cx<TwT>* __restrict__ tw) {
@@ -419,7 +356,7 @@ struct FftCT {
         const int kk = j % NS;
 #pragma unroll
         for (int r = 1; r < R; ++r)
-          v[k * R + r] = twm<S>(v[k * R + r], tw_elem<T>(tw[kk * r * (N / (NS * R))]));
+          v[k * R + r] = twm<S>(v[k * R + r], tw[kk * r * (N / (NS * R))]);
       }
       Dft<R, S, T>::run(&v[k * R]);
     }
@@ -438,14 +375,14 @@ struct FftCT {
       const int kk = j % NS;
       const int base = (j - kk) * R + kk;
 #pragma unroll
-      for (int r = 0; r < R; ++r) lds_put(&line[pad_index<T>(base + r * NS)], v[k * R + r]);
+      for (int r = 0; r < R; ++r) line[pad_index<T>(base + r * NS)] = v[k * R + r];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E / RN; ++k) {
       const int j = t + k * TP;
 #pragma unroll
-      for (int r = 0; r < RN; ++r) v[k * RN + r] = lds_get(&line[pad_index<T>(j + r * (N / RN))]);
+      for (int r = 0; r < RN; ++r) v[k * RN + r] = line[pad_index<T>(j + r * (N / RN))];
     }
   }
 
@@ -459,7 +396,7 @@ struct FftCT {
 #pragma unroll
       for (int r = 0; r < Sh::R0; ++r) {
         if constexpr (std::is_same<Load, NoLoad>::value)
-          v[k * Sh::R0 + r] = lds_get(&line[pad_index<T>(j + r * (N / Sh::R0))]);
+          v[k * Sh::R0 + r] = line[pad_index<T>(j + r * (N / Sh::R0))];
         else
           v[k * Sh::R0 + r] = load(b, j + r * (N / Sh::R0));
       }
@@ -508,7 +445,7 @@ struct FftCT {
     for (int k = 0; k < E / RL; ++k) {
       const int j = t + k * TP;
 #pragma unroll
-      for (int r = 0; r < RL; ++r) lds_put(&line[pad_index<T>(j + r * (N / RL))], v[k * RL + r]);
+      for (int r = 0; r < RL; ++r) line[pad_index<T>(j + r * (N / RL))] = v[k * RL + r];
     }
     __syncthreads();
   }
@@ -640,7 +577,7 @@ struct FftMR {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if constexpr (std::is_same<Load, NoLoad>::value)
-          v[k * R + r] = lds_get(&line[pad_index<T>(j + r * NB)]);
+          v[k * R + r] = line[pad_index<T>(j + r * NB)];
         else
           v[k * R + r] = load(b, j + r * NB);
       }
@@ -675,7 +612,7 @@ struct FftMR {
       const int kk = j % NS;
       const int base = (j - kk) * R + kk;
 #pragma unroll
-      for (int r = 0; r < R; ++r) lds_put(&line[pad_index<T>(base + r * NS)], v[k * R + r]);
+      for (int r = 0; r < R; ++r) line[pad_index<T>(base + r * NS)] = v[k * R + r];
     }
   }
 
@@ -729,7 +666,7 @@ struct FftMR {
       const int j = t + k * TP;
       if (!active<NP - 1>(j)) continue;
 #pragma unroll
-      for (int r = 0; r < RL; ++r) lds_put(&line[pad_index<T>(j + r * NB)], v[k * RL + r]);
+      for (int r = 0; r < RL; ++r) line[pad_index<T>(j + r * NB)] = v[k * RL + r];
     }
     __syncthreads();
   }

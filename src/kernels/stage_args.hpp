@@ -64,9 +64,6 @@ struct ColDesc {
   int nRuns;
 };
 
-__host__ __device__ inline long long inter_col(long long bStride, long long cStride, int c) {
-  return static_cast<long long>(c >> 3) * bStride + static_cast<long long>(c & 7) * cStride;
-}
 
 struct YArgs {
   int ncols;     // columns of the [z][column][y] intermediate (its row count per plane)
@@ -77,12 +74,8 @@ struct YArgs {
   int n;  // dimY
   int colOfX0;  // column needing the x=0 plane hermitian fill, -1 for none
   long long interStride;  // row stride of the [z][column][y] intermediate (>= n)
-  // row (z, column c) of the intermediate starts at
-  //   z * interZStride + (c / 8) * interBStride + (c % 8) * interCStride
-  // plane-major [z][c][y]:       ncols*S, 8*S,     S
-  // column-major [c][z][y]:      S,       8*L*S,   L*S
-  // blocked [c/8][z][c%8][y]:    8*S,     8*L*S,   S        (S = interStride)
-  long long interZStride, interBStride, interCStride;
+  // row (z, column c) of the intermediate starts at z * interZStride + c * interStride
+  long long interZStride;
   const int* colOffsets;
   const int* colY;
   const long long* colBase;
@@ -101,10 +94,17 @@ struct XArgs {
   int nFreq;  // dimX/2+1 for R2C, dimX for C2C
   int ncols;
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
-  long long interZStride, interBStride, interCStride;  // as YArgs
+  long long interZStride;  // as YArgs
   const int* colX;
   BatchPtrs batch;
 };
+
+// Offset of column c's row inside one plane of the intermediate (a plane holds
+// ncols * interStride < 2^31 elements: 32-bit arithmetic per lane).
+template <class A>
+__host__ __device__ inline int inter_row(const A& a, int c) {
+  return c * static_cast<int>(a.interStride);
+}
 
 // grid z extent of a launch (1 when unbatched)
 inline unsigned batch_dim(const BatchPtrs& b) { return b.count > 1 ? static_cast<unsigned>(b.count) : 1u; }

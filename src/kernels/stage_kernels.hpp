@@ -199,67 +199,6 @@ struct CtEng {
   static std::size_t h_lds() { return F::lds_bytes(); }
 };
 
-// Paired fp32 line-fast engine: the FFT core runs on cx<f2> (lines 2p and 2p+1
-// in one lane, packed fp32 arithmetic) while the stage kernels keep addressing
-// single complex<float> lines: lane pair p carries lines p and p + F::B, so each
-// load/store instruction of a wave covers the same contiguous line run as the
-// unpaired engine; the LDS tile keeps each pair as two adjacent complex<float>
-// values (lds_put/lds_get).
-#ifndef SPFFT_F32_PAIR
-#define SPFFT_F32_PAIR 0  // measured slower: profiles/r2_s1/pair_ab.txt
-#endif
-template <int N, int S>
-struct CtEngPair {
-  using F = FftCT<f2, N, S, true>;
-  static constexpr bool kBatchedCopy = false;
-  static constexpr bool kLineFast = true;
-  static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
-  __device__ int lines() const { return 2 * F::B; }
-  __device__ int n() const { return N; }
-  __device__ int in_at(int b, int pos) const { return 2 * F::in_at(b % F::B, pos) + b / F::B; }
-  __device__ int out_at(int b, int pos) const { return 2 * F::out_at(b % F::B, pos) + b / F::B; }
-  __device__ int input_elems() const { return 2 * F::B * F::LS; }
-  __device__ int lds_bytes() const { return static_cast<int>(F::lds_bytes()); }
-  static __device__ cx<f2>* pairs(cx<float>* lds) { return reinterpret_cast<cx<f2>*>(lds); }
-  template <class Ld>
-  static __device__ auto pair_load(Ld& ld) {
-    return [&](int p, int pos) -> cx<f2> {
-      const cx<float> a = ld(p, pos), b = ld(p + F::B, pos);
-      f2 re, im;
-      re.x = a.x;
-      re.y = b.x;
-      im.x = a.y;
-      im.y = b.y;
-      return mk<f2>(re, im);
-    };
-  }
-  template <class St>
-  static __device__ auto pair_store(St& st) {
-    return [&](int p, int pos, cx<f2> v) {
-      st(p, pos, mk<float>(v.x.x, v.y.x));
-      st(p + F::B, pos, mk<float>(v.x.y, v.y.y));
-    };
-  }
-  template <class St>
-  __device__ void lds_to_global(cx<float>* lds, const cx<float>* __restrict__ tw, St st) const {
-    F::run(pairs(lds), tw, NoLoad{}, pair_store(st));
-  }
-  template <class Ld>
-  __device__ void global_to_lds(cx<float>* lds, const cx<float>* __restrict__ tw, Ld ld) const {
-    F::run_to_lds(pairs(lds), tw, pair_load(ld));
-  }
-  __device__ void lds_to_lds(cx<float>* lds, const cx<float>* __restrict__ tw) const {
-    F::run_to_lds(pairs(lds), tw, NoLoad{});
-  }
-  template <class Ld, class St>
-  __device__ void global_to_global(cx<float>* lds, const cx<float>* __restrict__ tw, Ld ld, St st) const {
-    F::run(pairs(lds), tw, pair_load(ld), pair_store(st));
-  }
-  static int h_lines() { return 2 * F::B; }
-  static int h_threads() { return F::NT; }
-  static std::size_t h_lds() { return F::lds_bytes(); }
-};
-
 // Run-time length engine. LF (line-fast) engines walk the global side with the
 // line index fastest — consecutive lanes touch consecutive lines, i.e. the
 // contiguous z-run of a stick or y-run of an intermediate column — like the
@@ -600,50 +539,16 @@ __device__ __forceinline__ int find_run(const RunTable& t, int idx) {
   return lo;
 }
 
-// XCD-aware workgroup order (SPFFT_XCD_REMAP=1): the dispatcher deals
-// consecutive workgroups round-robin to the 8 XCDs; the remap gives XCD x the
-// contiguous tile range [x*n/8, (x+1)*n/8), so each XCD's L2 and its memory
-// requests see neighbouring tiles. 2D grids are linearised x-fastest.
-// Measured on MI355X at 256^3 (profiles/r2_s1/shape_ab.txt): x and y stages
-// 3-6 us slower, z stages 1-2 us faster, bench -4.5%. The stages have no
-// cross-workgroup reuse for an XCD's L2 to exploit, and the default
-// round-robin spreads the addresses in flight over all eight XCDs' paths to
-// HBM, so the remap stays off.
-#ifndef SPFFT_XCD_REMAP
-#define SPFFT_XCD_REMAP 0
-#endif
+// Workgroup -> tile mapping: the dispatcher deals consecutive workgroups
+// round-robin to the 8 XCDs. An XCD-contiguous remap was measured slower on
+// MI355X at 256^3 (x/y stages 3-6 us, bench -4.5%, profiles/r2_s1/shape_ab.txt):
+// the stages have no cross-workgroup reuse for an XCD's L2, and round-robin
+// spreads the addresses in flight over all eight XCDs' paths to HBM.
 __device__ __forceinline__ void block_tile(int& bx, int& by) {
   bx = blockIdx.x;
   by = blockIdx.y;
-#if SPFFT_XCD_REMAP
-  const int n = gridDim.x * gridDim.y;
-  if (n % 8 == 0) {
-    const int id = blockIdx.x + blockIdx.y * gridDim.x;
-    const int lin = (id % 8) * (n / 8) + id / 8;
-    bx = lin % gridDim.x;
-    by = lin / gridDim.x;
-  }
-#endif
 }
-__device__ __forceinline__ int block_tile_x() {
-  int bx, by;
-  block_tile(bx, by);
-  return bx;
-}
-
-// Reversed tile order for a stage that reads what the previous stage wrote
-// (SPFFT_REVERSE_READS bit mask): the most recently written data, the part
-// still held in the 256 MB memory-side Infinity Cache, is read first.
-//   1: y backward columns (z backward wrote the sticks column by column)
-//   2: x forward planes (x backward wrote the space planes in order)
-//   4: z forward sticks (y forward wrote the sticks column by column)
-#ifndef SPFFT_REVERSE_READS
-#define SPFFT_REVERSE_READS 0  // within noise: profiles/r2_s1/reverse_reads.txt
-#endif
-template <int Bit>
-__device__ __forceinline__ int tile_order(int t, int n) {
-  return (SPFFT_REVERSE_READS & Bit) ? n - 1 - t : t;
-}
+__device__ __forceinline__ int block_tile_x() { return blockIdx.x; }
 
 // Batched launch (ZArgs/YArgs/XArgs::batch): the workgroup's transform
 // (blockIdx.z) supplies the input and output buffers; the index tables are
@@ -714,7 +619,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_LDS_DECL(T);
   SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
-  const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
+  const int s0 = a.stickBegin + block_tile_x() * B;
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
@@ -808,7 +713,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_LDS_DECL(T);
   SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
-  const int s0 = a.stickBegin + tile_order<4>(block_tile_x(), gridDim.x) * B;
+  const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
@@ -891,13 +796,6 @@ __device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride
 // Every kernel keeps a single FFT call site whichever source is used: the
 // run-time engines inline their whole pass switch per call site, and a second
 // copy doubled their register demand (profiles/r2_s1/rt_regression.txt).
-// SPFFT_Y_BASE_TABLE=1: descriptor columns also get a y -> base table in LDS
-// (experiment: trades ~30 VALU instructions of run selects per element for one
-// LDS read; see profiles/r2_s3/f32/)
-#ifndef SPFFT_Y_BASE_TABLE
-#define SPFFT_Y_BASE_TABLE 0
-#endif
-constexpr long long kNoBase = -0x7fffffffffffffffLL - 1;
 template <class Eng>
 struct ColEntries {
   bool useDesc;
@@ -917,17 +815,6 @@ struct ColEntries {
     ne = 0;
     if (useDesc) {
       d = a.colDesc[c];
-#if SPFFT_Y_BASE_TABLE
-      // y -> base (or -1) once per workgroup: one LDS read per element instead
-      // of the per-element run selects
-      // miss sentinel LLONG_MIN: peer-write plans hold negative bases (offsets
-      // of a peer's buffer from the local one)
-      for (int y = threadIdx.x; y < n; y += blockDim.x) {
-        long long b;
-        cBase[y] = col_desc_find(d, stride, y, b) ? b : kNoBase;
-      }
-      __syncthreads();
-#endif
       return;
     }
     const int k0 = a.colOffsets[c];
@@ -944,14 +831,7 @@ struct ColEntries {
   }
   // whether the column has an entry at y; its base (add the plane) in base
   __device__ bool find(int y, long long& base) const {
-#if SPFFT_Y_BASE_TABLE
-    if (useDesc) {
-      base = cBase[y];
-      return base != kNoBase;
-    }
-#else
     if (useDesc) return col_desc_find(d, stride, y, base);
-#endif
     const int e = yEnt[y];
     base = e < 0 ? 0 : cBase[e];
     return e >= 0;
@@ -965,7 +845,7 @@ struct ColEntries {
 inline std::size_t col_entries_lds(const YArgs& a, bool backward) {
   const bool list = !a.colDesc || (backward && a.colOfX0 >= 0);
   if (list) return std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
-  return SPFFT_Y_BASE_TABLE ? std::size_t(a.n) * sizeof(long long) + 16 : 0;
+  return 0;
 }
 
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
@@ -980,7 +860,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, in, inter);
   const int B = eng.lines();
   const int n = eng.n();
-  const int c = a.colBegin + tile_order<1>(y_tile_col(), SPFFT_Y_ZFAST ? gridDim.y : gridDim.x);
+  const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   const bool x0 = c == a.colOfX0;
@@ -1025,7 +905,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return eng.out_at(b, idx - b * n);
   }, [&](int idx, cx<T> v) {
     const int b = idx / n;
-    st_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + idx - b * n], v);
+    st_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_row(a, c) + idx - b * n], v);
   });
 }
 
@@ -1046,7 +926,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const ColEntries<Eng> ce(eng, a, lds, c, true);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
-    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_col(a.interBStride, a.interCStride, c) + pos]);
+    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_row(a, c) + pos]);
   };
   auto store = [&](int b, int pos, cx<T> v) {
     long long base;
@@ -1110,10 +990,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (b >= yl) return czero<T>();
     if (R2C && pos >= a.nFreq) {
       const int c = xcol_of(a, xCol, n - pos);
-      return c < 0 ? czero<T>() : conj(ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]));
+      return c < 0 ? czero<T>() : conj(ld_inter(&src[inter_row(a, c) + b]));
     }
     const int c = xcol_of(a, xCol, pos);
-    return c < 0 ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
+    return c < 0 ? czero<T>() : ld_inter(&src[inter_row(a, c) + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
@@ -1141,7 +1021,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   int tx, ty;
   block_tile(tx, ty);
-  const int zl = a.zBegin + tile_order<2>(ty, gridDim.y);
+  const int zl = a.zBegin + ty;
   const int y0 = tx * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, n);
@@ -1155,7 +1035,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   };
   auto store = [&](int b, int pos, cx<T> v) {
     const int c = xcol_of(a, xCol, pos);
-    if (c >= 0 && b < yl) st_inter(&dst[inter_col(a.interBStride, a.interCStride, c) + b], v);
+    if (c >= 0 && b < yl) st_inter(&dst[inter_row(a, c) + b], v);
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
@@ -1200,7 +1080,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     // data, so its second read is served by the caches; plain loads keep it there)
     auto col = [&](int k, int b) -> cx<T> {
       const int c = xcol_of(a, xCol, k);
-      return (c < 0 || b >= yl) ? czero<T>() : src[inter_col(a.interBStride, a.interCStride, c) + b];
+      return (c < 0 || b >= yl) ? czero<T>() : src[inter_row(a, c) + b];
     };
     eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
       cx<T> xk = col(k, b);
@@ -1225,14 +1105,14 @@ __global__ void __launch_bounds__(Eng::kBlock)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
     const int k = idx / B, b = idx - k * B;
     const int c = xcol_of(a, xCol, k);
-    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
+    return (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_row(a, c) + b]);
   }, [&](int idx) {
     const int k = idx / B;
     return eng.in_at(idx - k * B, k);
   });
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int c = xcol_of(a, xCol, h);
-    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_col(a.interBStride, a.interCStride, c) + b]);
+    nyq[b] = (c < 0 || b >= yl) ? czero<T>() : ld_inter(&src[inter_row(a, c) + b]);
   }
   __syncthreads();
   // pre-pass in place, pairs (k, h-k): Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k
@@ -1270,7 +1150,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const long long n = 2 * static_cast<long long>(h);
   int tx, ty;
   block_tile(tx, ty);
-  const int zl = a.zBegin + tile_order<2>(ty, gridDim.y);
+  const int zl = a.zBegin + ty;
   const int y0 = tx * B;
   int* xCol = reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   build_xcol(a, xCol, h + 1);
@@ -1297,7 +1177,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
     const cx<T> e = scale(yk + ym, T(0.5));
     const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
-    st_inter(&dst[inter_col(a.interBStride, a.interCStride, c) + b], e + twm<-1>(o, twn[k]));
+    st_inter(&dst[inter_row(a, c) + b], e + twm<-1>(o, twn[k]));
   }
 }
 
@@ -1332,14 +1212,8 @@ inline void with_engine(int n, F&& f) {
   switch (n) {
 #define SPFFT_CT_CASE(NN)                                                         \
   case NN: {                                                                      \
-    if constexpr (SPFFT_F32_PAIR && LF && std::is_same<T, float>::value &&          \
-                  NN >= 64 && (NN & (NN - 1)) == 0) {                             \
-      using E = CtEngPair<NN, S>;                                                 \
-      f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                           \
-    } else {                                                                      \
-      using E = CtEng<T, NN, S, LF>;                                              \
-      f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                           \
-    }                                                                             \
+    using E = CtEng<T, NN, S, LF>;                                                \
+    f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                             \
     return;                                                                       \
   }
     SPFFT_CT_CASE(16)

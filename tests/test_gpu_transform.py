@@ -542,30 +542,6 @@ def test_nan_poison(gpu, dims, ttype, monkeypatch):
     assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims, r2c=r2c)) < 1e-12
 
 
-@pytest.mark.parametrize("n", [64, 128])
-def test_fused_xcd_path(gpu, n, monkeypatch):
-    """Opt-in fused path (SPFFT_FUSED=1): plane-major sticks, persistent XCD-cooperative
-    y/x kernels with an L2 plane ring; checked against torch.fft, repeated with fresh
-    data (a stale ring buffer would show up on the second round)."""
-    import torch
-    monkeypatch.setenv("SPFFT_FUSED", "1")
-    dims = (n, n, n)
-    idx = sphere_indices(*dims, 0.5)
-    grid = sp.Grid(n, n, n, n * n, GPU, 1)
-    t = grid.create_transform(GPU, sp.TransformType.C2C, n, n, n, n, idx)
-    s = torch.as_tensor(np.where(idx < 0, idx + n, idx).astype(np.int64), device=gpu)
-    for seed in (1, 2):
-        rng = np.random.default_rng(seed)
-        vals = torch.as_tensor(_rand_vals(rng, len(idx)), device=gpu)
-        out = t.backward(vals)
-        F = torch.zeros((n, n, n), dtype=torch.complex128, device=gpu)
-        F[s[:, 0], s[:, 1], s[:, 2]] = vals
-        ref = (torch.fft.ifftn(F) * n ** 3).permute(2, 1, 0)
-        assert ((out - ref).abs().max() / ref.abs().max()).item() < 1e-12
-        f = t.forward(None, scaling=sp.Scaling.FULL)
-        assert ((f - vals).abs().max() / vals.abs().max()).item() < 1e-12
-
-
 @pytest.mark.parametrize("dims,r2c,single", [((67, 8, 101), False, False), ((127, 3, 2), False, False),
                                              ((103, 16, 67), True, False), ((2, 257, 5), False, True),
                                              ((1021, 2, 3), False, False), ((97, 89, 4), True, True)])
