@@ -117,19 +117,30 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
       upload(segDispl_, sdl);
       bwdSendCounts_[p.rank] = bwdRecvCounts_[p.rank] = 0;
     }
-    // exchange pipelining over plane chunks (build_chunk_plan). Automatic
-    // choice: chunks only while the average per-peer message of a chunk stays
-    // >= 4 MB (smaller RCCL messages lose link efficiency), at most 4; computed
-    // from global quantities so every rank agrees. SPFFT_EXCH_CHUNKS forces a
-    // count (rank 0's value is used everywhere).
+    // Exchange pipelining over plane chunks (build_chunk_plan): chunk k's
+    // all-to-all overlaps the y/x stages of chunk k-1 (backward) or k+1
+    // (forward). Model: a chunk pays one grouped send/recv launch (~10-20 us
+    // of fixed cost) and per-peer messages below ~1.5 MB lose link efficiency,
+    // so K = per-peer bytes / 1.5 MB, between 1 and 4. 256^3 C2C fp64 sends
+    // 3.3 MB per peer at P = 8 (K = 2), 13 MB at P = 4 and 53 MB at P = 2
+    // (K = 4). Computed from global quantities so every rank agrees;
+    // SPFFT_EXCH_CHUNKS forces a count (rank 0's value is used everywhere).
+    // The peer-write plane needs none: its stores are issued by the stage
+    // kernels themselves and overlap their compute wave by wave.
     const double perPeer = static_cast<double>(p.totalSticks) * p.dimZ * eb /
                            (static_cast<double>(p.size) * p.size);
-    int chunks = static_cast<int>(std::min(4.0, std::max(1.0, std::floor(perPeer / (4 << 20)))));
+    chunkModel_ = perPeer;
+    int chunks = static_cast<int>(std::min(4.0, std::max(1.0, std::floor(perPeer / (1.5 * (1 << 20))))));
     chunks = env_int("SPFFT_EXCH_CHUNKS", chunks, 1, 64);
-    std::vector<int> all(p.size);
-    grid_->communicator()->allgather(&chunks, all.data(), sizeof(int));
+    if (peerWrites_) chunks = 1;
+    // rank 0's count, reduced until the (padded) layout fits every rank's buffers
+    int req[2] = {chunks, 1};
+    while (req[1] < chunks && chunk_plan_fits(req[1] + 1)) ++req[1];
+    std::vector<int> all(2 * p.size);
+    grid_->communicator()->allgather(req, all.data(), sizeof(req));
     chunks = all[0];
-    if (!peerWrites_ && chunks > 1) build_chunk_plan(chunks);
+    for (int r = 0; r < p.size; ++r) chunks = std::min(chunks, all[2 * r + 1]);
+    if (chunks > 1 && !build_chunk_plan(chunks)) throw InternalError();
   }
   log_plan();
 }
@@ -146,7 +157,8 @@ void GpuExecutor<T>::log_plan() const {
   if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
-               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d peer_writes=%d\n",
+               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d (%.2f MB per peer) "
+               "peer_writes=%d\n",
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
@@ -154,7 +166,8 @@ void GpuExecutor<T>::log_plan() const {
                dev::describe_engine(p.dimY, dbl, true).c_str(),
                dev::describe_engine(twXh_ ? p.dimX / 2 : p.dimX, dbl, true).c_str(),
                twXh_ ? " packed-real" : "", layout_.buffered ? "buffered" : "compact",
-               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, peerWrites_ ? 1 : 0);
+               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, chunkModel_ / 1e6,
+               peerWrites_ ? 1 : 0);
 }
 
 template <typename T>
@@ -194,18 +207,38 @@ void GpuExecutor<T>::build_col_desc(ColDescTable& t, const std::vector<long long
   upload(t.buf, d);
 }
 
+// Chunk plan of the pipelined exchange. Both exchange buffers are laid out
+// chunk-major: segment v = k*P + r of the stick side holds (local sticks) x
+// (chunk k of rank r's planes), block (k, q) of the slab side holds (sticks of
+// rank q) x (chunk k of my planes), so chunk k is one contiguous block per peer
+// on both sides. BUFFERED pads every block to maxSticks rows of
+// ceil(maxPlanes / K) planes (equal counts, the reference's MPI_Alltoall
+// shape); compact blocks are exact. Returns false when the padded layout does
+// not fit the grid's exchange buffers (the caller tries fewer chunks).
 template <typename T>
-void GpuExecutor<T>::build_chunk_plan(int K) {
+bool GpuExecutor<T>::chunk_plan_fits(int K) const {
+  const IndexPlan& p = *plan_;
+  if (!layout_.buffered) return true;  // compact chunks only reorder the blocks
+  const i64 Mk = (static_cast<i64>(p.maxPlanes) + K - 1) / K;
+  const i64 need = static_cast<i64>(K) * p.size * p.maxSticks * Mk;
+  return need <= grid_->slot_elements(GridImpl<T>::kStickSide) &&
+         need <= grid_->slot_elements(GridImpl<T>::kSlabSide);
+}
+
+template <typename T>
+bool GpuExecutor<T>::build_chunk_plan(int K) {
   const IndexPlan& p = *plan_;
   const int P = p.size, me = p.rank;
   // K depends on global quantities only: every rank issues the same number of
   // all-to-all rounds (a rank with fewer planes than K gets empty chunks)
-  if (layout_.buffered || K < 2) return;
+  if (K < 2) return false;
+  const bool buf = layout_.buffered;
   const i64 eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   auto pb = [&](int r, int k) -> i64 { return static_cast<i64>(p.planesPerRank[r]) * k / K; };
   const i64 S = p.local_sticks();
-  // stick side: segment v = k*P + r holds (local sticks) x (chunk k of rank r's
-  // planes); the z stage finds a plane's segment through the zRank table
+  const i64 Mk = (static_cast<i64>(p.maxPlanes) + K - 1) / K;  // padded chunk (BUFFERED)
+  const i64 rowsPad = p.maxSticks;
+  auto stride = [&](int r, int k) -> i64 { return buf ? Mk : pb(r, k + 1) - pb(r, k); };
   const int NV = K * P;
   std::vector<long long> segDispl(NV), segStride(NV);
   std::vector<int> segZOff(NV), zSeg(p.dimZ, 0);
@@ -215,46 +248,45 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
       const int v = k * P + r;
       const i64 n = pb(r, k + 1) - pb(r, k);
       segDispl[v] = off;
-      segStride[v] = n;
+      segStride[v] = stride(r, k);
       segZOff[v] = p.planeOffsets[r] + static_cast<int>(pb(r, k));
       for (i64 z = 0; z < n; ++z) zSeg[segZOff[v] + z] = v;
-      off += S * n;
+      off += (buf ? rowsPad : S) * segStride[v];
     }
   }
-  if (off != layout_.stickTotal) throw InternalError();
-  // slab side: block (k, q) holds (sticks of rank q) x (chunk k of my planes)
+  if (off > grid_->slot_elements(GridImpl<T>::kStickSide)) return false;
   std::vector<i64> slabDispl(NV);
-  off = 0;
+  i64 soff = 0;
   for (int k = 0; k < K; ++k) {
-    const i64 lk = pb(me, k + 1) - pb(me, k);
     for (int q = 0; q < P; ++q) {
-      slabDispl[k * P + q] = off;
-      off += static_cast<i64>(p.sticksPerRank[q]) * lk;
+      slabDispl[k * P + q] = soff;
+      soff += (buf ? rowsPad : static_cast<i64>(p.sticksPerRank[q])) * stride(me, k);
     }
   }
-  if (off != layout_.slabTotal) throw InternalError();
+  if (soff > grid_->slot_elements(GridImpl<T>::kSlabSide)) return false;
+  if (!buf && (off != layout_.stickTotal || soff != layout_.slabTotal)) throw InternalError();
   planeBounds_.resize(K + 1);
   for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
   colBaseChunk_.clear();
   colDescChunk_.clear();
   chunks_.assign(K, ChunkXfer{});
   for (int k = 0; k < K; ++k) {
-    const i64 lk = pb(me, k + 1) - pb(me, k);
+    const i64 sk = stride(me, k);
     // entry e at local plane z of chunk k: base + z (z in [pb_k, pb_k+1))
     std::vector<long long> cb(p.colY.size());
     for (std::size_t e = 0; e < p.colY.size(); ++e)
-      cb[e] = slabDispl[k * P + p.colRank[e]] + static_cast<i64>(p.colLocal[e]) * lk - pb(me, k);
+      cb[e] = slabDispl[k * P + p.colRank[e]] + static_cast<i64>(p.colLocal[e]) * sk - pb(me, k);
     colBaseChunk_.emplace_back();
     upload(colBaseChunk_.back(), cb);
     colDescChunk_.emplace_back();
-    build_col_desc(colDescChunk_.back(), cb, lk);
+    build_col_desc(colDescChunk_.back(), cb, sk);
     ChunkXfer& c = chunks_[k];
     for (int r = 0; r < P; ++r) {
       const int v = k * P + r;
       c.sd.push_back(segDispl[v] * eb);
-      c.sc.push_back(S * segStride[v] * eb);
+      c.sc.push_back((buf ? rowsPad : S) * segStride[v] * eb);
       c.rd.push_back(slabDispl[v] * eb);
-      c.rc.push_back(static_cast<i64>(p.sticksPerRank[r]) * lk * eb);
+      c.rc.push_back((buf ? rowsPad : static_cast<i64>(p.sticksPerRank[r])) * sk * eb);
     }
     if (localDirect_) {
       // own block in place on the slab side (see the constructor)
@@ -272,6 +304,7 @@ void GpuExecutor<T>::build_chunk_plan(int K) {
   for (int k = 0; k < K; ++k) chunkEvents_.emplace_back(new GpuEvent());
   commDone_.reset(new GpuEvent());
   zDone_.reset(new GpuEvent());
+  return true;
 }
 
 // Element offset (exchange element type) from the stick-side buffer to the

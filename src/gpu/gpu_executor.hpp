@@ -74,7 +74,8 @@ private:
   void order_after_default_stream();
   void exchange(bool backward);
   void build_peer_tables();
-  void build_chunk_plan(int chunks);
+  bool build_chunk_plan(int chunks);
+  bool chunk_plan_fits(int chunks) const;
   void pipelined_exchange(bool backward);
   void wait_stream();
   void wait_stream_watched();
@@ -167,6 +168,7 @@ private:
     std::vector<std::int64_t> sc, sd, rc, rd;  // bytes per rank (backward direction)
   };
   int exchChunks_ = 1;
+  double chunkModel_ = 0;  // per-peer bytes of one exchange (chunk model input)
   std::vector<int> planeBounds_;  // K+1 local plane bounds of the chunks
   std::vector<ChunkXfer> chunks_;
   std::vector<std::unique_ptr<DeviceBuffer>> colBaseChunk_;  // y-stage entry bases per chunk

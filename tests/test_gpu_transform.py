@@ -751,11 +751,15 @@ def test_long_lines(gpu, dims, single, ttype):
         assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims)) < tol
 
 
-@pytest.mark.parametrize("P,chunks", [(8, 1), (8, 2), (4, 3), (2, 4)])
-def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, monkeypatch):
+@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "COMPACT_BUFFERED_FLOAT", "BUFFERED",
+                                      "BUFFERED_FLOAT", "UNBUFFERED"])
+@pytest.mark.parametrize("P,chunks", [(8, 1), (8, 2), (8, 4), (4, 3), (2, 4)])
+def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, exchange, monkeypatch):
     """The driver's scaling configurations (2/4/8 ranks, the chunk counts the automatic
     rule picks at 256^3) on virtual ranks of one GPU, with a sphere split evenly like
-    bench.py: multi_transform of 2 transforms per rank, backward vs numpy, round trip."""
+    bench.py, for every exchange type (BUFFERED chunks are padded blocks; UNBUFFERED
+    uses peer writes, which are never chunked): multi_transform of 2 transforms per
+    rank, backward vs numpy, round trip."""
     import torch
     from spfft_amd.parallel import TorchDistComm, make_distributed, run_ranks  # noqa: F401
     from spfft_amd.utils.indices import distribute_sticks
@@ -777,7 +781,7 @@ def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, monkeypatch):
         ts = []
         for _ in range(2):
             g = sp.Grid(nx, ny, nz, max_sticks, GPU, 1, max_local_z_length=max(planes), comm=comm,
-                        exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+                        exchange_type=getattr(sp.ExchangeType, exchange))
             ts.append(g.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
                                          parts[rank]))
         ins = [torch.as_tensor(v[starts[rank]:starts[rank + 1]], device="cuda") for v in vals]
@@ -788,8 +792,9 @@ def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, monkeypatch):
         e2 = max(max_rel_error(b.cpu().numpy(), i.cpu().numpy()) for b, i in zip(back, ins))
         return max(e, e2)
 
+    tol = 1e-5 if exchange.endswith("FLOAT") else 1e-11
     for e in run_ranks(P, body):
-        assert e < 1e-11
+        assert e < tol
 
 
 # ------------------------------------------------------------ RCCL data plane
@@ -866,7 +871,7 @@ def test_rccl_channel_shared_across_grids(gpu, monkeypatch):
         ts = []
         for _ in range(3):
             g = sp.Grid(nx, ny, nz, max_sticks, GPU, 1, max_local_z_length=max(planes), comm=comm,
-                        exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+                        exchange_type=getattr(sp.ExchangeType, exchange))
             ts.append(g.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
                                          parts[rank]))
         ins = [torch.as_tensor(v[starts[rank]:starts[rank + 1]], device="cuda") for v in vals]
