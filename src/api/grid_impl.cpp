@@ -1,6 +1,7 @@
 #include "api/grid_impl.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <thread>
 #include <vector>
@@ -38,6 +39,13 @@ void GridImpl<T>::init(int maxDimX, int maxDimY, int maxDimZ, int maxSticks, int
   // room for row / stick padding (kMaxPad elements per row or stick)
   planeElems_ = checked_mul(checked_mul(maxX_, maxY_ + kMaxPad), std::max(1, maxLocalZ_));
   exchElems_ = std::max(planeElems_, checked_mul(maxZ_ + kMaxPad, maxSticks_));
+  {
+    const char* e = std::getenv("SPFFT_INTER_BYTES");
+    const double capBytes = e && *e ? std::atof(e) : 2.0 * (1 << 30);
+    const i64 onePlane = checked_mul(maxX_, maxY_ + kMaxPad);
+    const i64 cap = static_cast<i64>(capBytes / (2.0 * sizeof(T)));
+    interDevElems_ = std::min(planeElems_, std::max(onePlane, cap));
+  }
   if (pu_ & SPFFT_PU_GPU) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
@@ -107,7 +115,8 @@ GridImpl<T>::GridImpl(const GridImpl& o)
       exchange_(o.exchange_),
       comm_(o.comm_ ? o.comm_->duplicate() : nullptr),
       exchElems_(o.exchElems_),
-      planeElems_(o.planeElems_) {
+      planeElems_(o.planeElems_),
+      interDevElems_(o.interDevElems_) {
   if (pu_ & SPFFT_PU_GPU) {
     DeviceGuard guard(deviceId_);
     allocate_device();
@@ -139,7 +148,7 @@ void GridImpl<T>::allocate_device() {
   const std::size_t cb = sizeof(T) * 2;
   dev_[kStickSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
   if (!local()) dev_[kSlabSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
-  dev_[kInter].reset(new DeviceBuffer(static_cast<std::size_t>(planeElems_) * cb));
+  dev_[kInter].reset(new DeviceBuffer(static_cast<std::size_t>(interDevElems_) * cb));
   dev_[kSpace].reset(new DeviceBuffer(static_cast<std::size_t>(planeElems_) * cb));
 }
 

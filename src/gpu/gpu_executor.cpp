@@ -53,6 +53,14 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
+  {
+    // plane ranges of the y/x stages that fit the grid's (capped) intermediate
+    const long long perPlane = static_cast<long long>(p.num_columns()) * interStride_;
+    if (perPlane >= (1LL << 31)) throw InvalidParameterError();  // 32-bit row offsets
+    const int L = std::max(p.local_planes(), 1);
+    const long long cap = grid_->device_slot_elements(GridImpl<T>::kInter);
+    interPlanes_ = perPlane > 0 ? static_cast<int>(std::min<long long>(L, std::max(1LL, cap / perPlane))) : L;
+  }
   for (int n : {p.dimX, p.dimY, p.dimZ}) {
     if (!dev::has_ct_kernel(n) && n > dev::max_device_fft_length(sizeof(T) == 8))
       throw GPUFFTError();
@@ -157,15 +165,15 @@ void GpuExecutor<T>::log_plan() const {
   if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
-               "y{%s} x{%s}%s | exchange=%s%s plane=%s chunks=%d (%.2f MB per peer) "
-               "peer_writes=%d\n",
+               "y{%s} x{%s}%s inter_planes=%d | exchange=%s%s plane=%s chunks=%d (%.2f MB per "
+               "peer) peer_writes=%d\n",
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
                dev::describe_engine(p.dimZ, dbl, false).c_str(),
                dev::describe_engine(p.dimY, dbl, true).c_str(),
                dev::describe_engine(twXh_ ? p.dimX / 2 : p.dimX, dbl, true).c_str(),
-               twXh_ ? " packed-real" : "", layout_.buffered ? "buffered" : "compact",
+               twXh_ ? " packed-real" : "", interPlanes_, layout_.buffered ? "buffered" : "compact",
                floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, chunkModel_ / 1e6,
                peerWrites_ ? 1 : 0);
 }
@@ -716,7 +724,7 @@ void GpuExecutor<T>::poison(bool backward) {
   if (!poison_ || capturing_) return;
   auto fill = [&](typename GridImpl<T>::Slot slot) {
     gpu_check(hipMemsetAsync(grid_->device_slot(slot), 0xFF,
-                             static_cast<std::size_t>(grid_->slot_elements(slot)) * sizeof(cx<T>),
+                             static_cast<std::size_t>(grid_->device_slot_elements(slot)) * sizeof(cx<T>),
                              stream_),
               "hipMemsetAsync");
   };
@@ -801,6 +809,15 @@ void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   exchange(true);
 }
 
+// The intermediate as seen by the y/x kernels of a plane range starting at z0:
+// they address plane z at z * interZStride, so a capped buffer is shifted to
+// hold planes [z0, z0 + interPlanes_).
+template <typename T>
+cx<T>* GpuExecutor<T>::inter_for(cx<T>* inter, int z0) const {
+  if (interPlanes_ >= plan_->local_planes()) return inter;
+  return inter - static_cast<long long>(z0) * plan_->num_columns() * interStride_;
+}
+
 template <typename T>
 void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   SPFFT_TIMED_SCOPE("gpu_backward_xy");
@@ -812,27 +829,32 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
-  // pipelined exchange: the y/x stages of chunk k start when it has arrived
+  // pipelined exchange: the y/x stages of chunk k start when it has arrived;
+  // within a chunk, plane ranges of at most interPlanes_ reuse the intermediate
   const int K = exchChunks_ > 1 ? exchChunks_ : 1;
   for (int k = 0; k < K; ++k) {
-    auto ya = yargs();
-    auto xa = xargs();
-    if (K > 1) {
-      chunkEvents_[k]->wait_on(stream_);
-      ya.zBegin = xa.zBegin = planeBounds_[k];
-      ya.L = xa.L = planeBounds_[k + 1];
-      if (ya.L <= ya.zBegin) continue;
-      ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
-      set_col_desc(ya, colDescChunk_[k]);
+    if (K > 1) chunkEvents_[k]->wait_on(stream_);
+    const int zb = K > 1 ? planeBounds_[k] : 0;
+    const int ze = K > 1 ? planeBounds_[k + 1] : plan_->local_planes();
+    for (int z0 = zb; z0 < ze; z0 += interPlanes_) {
+      auto ya = yargs();
+      auto xa = xargs();
+      ya.zBegin = xa.zBegin = z0;
+      ya.L = xa.L = std::min(ze, z0 + interPlanes_);
+      if (K > 1) {
+        ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
+        set_col_desc(ya, colDescChunk_[k]);
+      }
+      cx<T>* in = inter_for(inter, z0);
+      if (floatExchange_)
+        dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), in,
+                                             twY_->data<cx<T>>(), stream_);
+      else
+        dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), in,
+                                         twY_->data<cx<T>>(), stream_);
+      dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, in, space, twX_->data<cx<T>>(),
+                                twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
     }
-    if (floatExchange_)
-      dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
-                                           twY_->data<cx<T>>(), stream_);
-    else
-      dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter,
-                                       twY_->data<cx<T>>(), stream_);
-    dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, inter, space, twX_->data<cx<T>>(),
-                              twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
   }
   if (outputLocation == SPFFT_PU_HOST) {
     gpu_check(hipMemcpyAsync(grid_->host_slot(GridImpl<T>::kSpace), space, space_bytes(),
@@ -862,29 +884,33 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   // the y stage stores straight into the peers' stick sides
   if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
-  // pipelined exchange: chunk k's all-to-all starts when its y stage is done
+  // pipelined exchange: chunk k's all-to-all starts when its y stage is done;
+  // within a chunk, plane ranges of at most interPlanes_ reuse the intermediate
   const int K = exchChunks_ > 1 ? exchChunks_ : 1;
   for (int k = 0; k < K; ++k) {
-    auto ya = yargs();
-    auto xa = xargs();
-    if (K > 1) {
-      ya.zBegin = xa.zBegin = planeBounds_[k];
-      ya.L = xa.L = planeBounds_[k + 1];
-      ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
-      set_col_desc(ya, colDescChunk_[k]);
-    } else if (peerWrites_) {
-      ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
-      set_col_desc(ya, colDescRemote_);
-      ya.remote = 1;
-    }
-    if (ya.L > ya.zBegin) {
-      dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, inter, twX_->data<cx<T>>(),
+    const int zb = K > 1 ? planeBounds_[k] : 0;
+    const int ze = K > 1 ? planeBounds_[k + 1] : plan_->local_planes();
+    for (int z0 = zb; z0 < ze; z0 += interPlanes_) {
+      auto ya = yargs();
+      auto xa = xargs();
+      ya.zBegin = xa.zBegin = z0;
+      ya.L = xa.L = std::min(ze, z0 + interPlanes_);
+      if (K > 1) {
+        ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
+        set_col_desc(ya, colDescChunk_[k]);
+      } else if (peerWrites_) {
+        ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
+        set_col_desc(ya, colDescRemote_);
+        ya.remote = 1;
+      }
+      cx<T>* out = inter_for(inter, z0);
+      dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, out, twX_->data<cx<T>>(),
                                twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
       if (floatExchange_)
-        dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab),
+        dev::launch_y_forward<T, cx<float>>(ya, out, static_cast<cx<float>*>(slab),
                                             twY_->data<cx<T>>(), stream_);
       else
-        dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
+        dev::launch_y_forward<T, cx<T>>(ya, out, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
                                         stream_);
     }
     if (K > 1) chunkEvents_[k]->record(stream_);
@@ -981,7 +1007,7 @@ void GpuExecutor<T>::compute_batch_key() {
 template <typename T>
 bool GpuExecutor<T>::batchable() const {
   return batchEnabled_ && plan_->size == 1 && !peerWrites_ && exchChunks_ <= 1 && !capturing_ &&
-         !poison_;
+         !poison_ && interPlanes_ >= plan_->local_planes();
 }
 
 // A member needs no stream join when it runs on the leader's stream, or when

@@ -103,6 +103,8 @@ private:
   ExchangeLayout layout_;
   bool floatExchange_ = false;
   long long interStride_ = 0;  // row stride of [z][column][y]
+  int interPlanes_ = 1;        // planes per y/x launch pair (fits the grid's intermediate)
+  cx<T>* inter_for(cx<T>* inter, int z0) const;
   bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;
 

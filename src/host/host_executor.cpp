@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "core/timing.hpp"
 #include "spfft/exceptions.hpp"
@@ -15,19 +16,24 @@ inline bool nonzero(const cx<T>& v) {
   return v.x != T(0) || v.y != T(0);
 }
 
-// Hermitian completion of one line, only where the mirrored source is non-zero,
-// in the two half passes of the reference (src/symmetry/symmetry_host.hpp:43-94).
-template <typename T>
-void hermitian_fill(cx<T>* v, int n) {
-  for (int k = 1; k <= n / 2; ++k)
-    if (nonzero(v[k])) v[n - k] = conj(v[k]);
-  for (int k = n / 2 + 1; k < n; ++k)
-    if (nonzero(v[k])) v[n - k] = conj(v[k]);
-}
-
 template <typename To, typename From>
 inline cx<To> cvt(const cx<From>& v) {
   return mk<To>(static_cast<To>(v.x), static_cast<To>(v.y));
+}
+
+// Hermitian completion of lane l of a batch line, only where the mirrored
+// source is non-zero, in the two half passes of the reference
+// (src/symmetry/symmetry_host.hpp:43-94).
+template <typename T>
+void hermitian_lane(typename HostSimd<T>::VC* a, int n, int l) {
+  for (int k = 1; k <= n / 2; ++k) {
+    const cx<T> v = lane<T>(a[k], l);
+    if (nonzero(v)) set_lane<T>(a[n - k], l, conj(v));
+  }
+  for (int k = n / 2 + 1; k < n; ++k) {
+    const cx<T> v = lane<T>(a[k], l);
+    if (nonzero(v)) set_lane<T>(a[n - k], l, conj(v));
+  }
 }
 
 }  // namespace
@@ -36,132 +42,387 @@ template <typename T>
 HostExecutor<T>::HostExecutor(std::shared_ptr<GridImpl<T>> grid,
                               std::shared_ptr<const IndexPlan> plan)
     : grid_(std::move(grid)), plan_(std::move(plan)) {
-  const bool distributed = plan_->size > 1;
-  layout_ = make_exchange_layout(*plan_, distributed && is_exchange_buffered(grid_->exchange_type()));
+  const IndexPlan& p = *plan_;
+  const bool distributed = p.size > 1;
+  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()));
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
-  fftX_ = HostFft<T>(plan_->dimX);
-  fftY_ = HostFft<T>(plan_->dimY);
-  fftZ_ = HostFft<T>(plan_->dimZ);
+  // packed-real x stage (R2C, even dimX): one half-length complex FFT per row
+  packedReal_ = p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 2;
+  fftX_ = Fft(packedReal_ ? p.dimX / 2 : p.dimX);
+  fftY_ = Fft(p.dimY);
+  fftZ_ = Fft(p.dimZ);
+  twX_ = make_twiddles<T>(p.dimX);
+  // fused y/x per plane block when the blocks keep every thread busy and the
+  // block buffer stays cache-sized (SPFFT_HOST_FUSE=0/1 forces)
+  {
+    const int threads = grid_->pool().num_threads();
+    const i64 blocks = (p.local_planes() + W - 1) / W;
+    const std::size_t blockBytes = static_cast<std::size_t>(p.num_columns()) * p.dimY * sizeof(VC);
+    fuseXY_ = blocks >= 2 * threads && blockBytes <= (std::size_t(8) << 20);
+    const char* e = std::getenv("SPFFT_HOST_FUSE");
+    if (e && *e) fuseXY_ = e[0] == '1';
+  }
   scratch_.resize(grid_->pool().num_threads());
 }
 
 template <typename T>
-cx<T>* HostExecutor<T>::scratch(int thread, std::size_t n) {
+typename HostExecutor<T>::VC* HostExecutor<T>::scratch(int thread, std::size_t n) {
   auto& s = scratch_[thread];
   if (s.size() < n) s.resize(n);
   return s.data();
+}
+
+// W lines of a batch through `f` (a: n batch elements, b: n scratch elements);
+// lengths without a batched plan run the scalar engine lane by lane.
+template <typename T>
+void HostExecutor<T>::fft(const Fft& f, VC* a, VC* b, int nl, int sign) {
+  if (f.batched()) {
+    f.run(a, b, sign);
+    return;
+  }
+  const int n = f.size();
+  const HostFft<T>& s = f.scalar();
+  std::vector<cx<T>> line(n), work(s.scratch_size());
+  for (int l = 0; l < nl; ++l) {
+    for (int i = 0; i < n; ++i) line[i] = lane<T>(a[i], l);
+    s.execute(line.data(), 1, line.data(), 1, sign, work.data());
+    for (int i = 0; i < n; ++i) set_lane<T>(a[i], l, line[i]);
+  }
 }
 
 // ---------------------------------------------------------------- backward
 template <typename T>
 template <typename BT>
 void HostExecutor<T>::z_backward(const cx<T>* values, BT* stick) {
+  SPFFT_TIMED_SCOPE("z_fft");
   const IndexPlan& p = *plan_;
   const int Z = p.dimZ;
   const bool r2c = p.type == SPFFT_TRANS_R2C;
-  grid_->pool().parallel_for(p.local_sticks(), 16, [&](i64 b, i64 e, int t) {
-    cx<T>* buf = scratch(t, static_cast<std::size_t>(Z) + fftZ_.scratch_size());
-    cx<T>* fs = buf + Z;
-    for (i64 s = b; s < e; ++s) {
-      std::fill(buf, buf + Z, mk<T>(T(0), T(0)));
-      for (int q = p.stickRunOffsets[s]; q < p.stickRunOffsets[s + 1]; ++q) {
-        const StickRun& r = p.runs[q];
-        std::copy(values + r.valueStart, values + r.valueStart + r.length, buf + r.zStart);
+  const i64 S = p.local_sticks();
+  grid_->pool().parallel_for((S + W - 1) / W, 4, [&](i64 b, i64 e, int t) {
+    VC* a = scratch(t, block_scratch());
+    VC* w = a + Z;
+    for (i64 blk = b; blk < e; ++blk) {
+      const i64 s0 = blk * W;
+      const int nl = static_cast<int>(std::min<i64>(W, S - s0));
+      std::fill(a, a + Z, vzero<T>());
+      for (int l = 0; l < nl; ++l) {
+        const i64 s = s0 + l;
+        for (int q = p.stickRunOffsets[s]; q < p.stickRunOffsets[s + 1]; ++q) {
+          const StickRun& r = p.runs[q];
+          for (int j = 0; j < r.length; ++j) set_lane<T>(a[r.zStart + j], l, values[r.valueStart + j]);
+        }
+        if (r2c && s == p.zeroStick) hermitian_lane<T>(a, Z, l);
       }
-      if (r2c && s == p.zeroStick) hermitian_fill(buf, Z);
-      fftZ_.execute(buf, 1, buf, 1, +1, fs);
-      for (int r = 0; r < p.size; ++r) {
-        BT* dst = stick + layout_.stickDispl[r] + s * layout_.stickStride[r];
-        const cx<T>* src = buf + p.planeOffsets[r];
-        for (int z = 0; z < p.planesPerRank[r]; ++z) dst[z] = cvt<typename BT::value_type>(src[z]);
+      fft(fftZ_, a, w, nl, +1);
+      for (int l = 0; l < nl; ++l) {
+        const i64 s = s0 + l;
+        for (int r = 0; r < p.size; ++r) {
+          BT* dst = stick + layout_.stickDispl[r] + s * layout_.stickStride[r];
+          const VC* src = a + p.planeOffsets[r];
+          for (int z = 0; z < p.planesPerRank[r]; ++z)
+            dst[z] = cvt<typename BT::value_type>(lane<T>(src[z], l));
+        }
       }
     }
   });
 }
 
+// ------------------------------------------------------- y and x line sets
+// Column c's y-lines of planes z0 .. z0+nl-1 (one batch) from the slab side:
+// a stick entry's W plane values are contiguous there. Result in a[0..Y).
 template <typename T>
 template <typename BT>
-void HostExecutor<T>::y_backward(const BT* slab, cx<T>* inter) {
+void HostExecutor<T>::y_col_backward(const BT* slab, int c, int z0, int nl, VC* a, VC* w) {
   const IndexPlan& p = *plan_;
-  const int Y = p.dimY, L = p.local_planes(), C = p.num_columns();
-  const bool r2c = p.type == SPFFT_TRANS_R2C;
-  grid_->pool().parallel_for(static_cast<i64>(C) * L, std::max(1, L / 4), [&](i64 b, i64 e, int t) {
-    cx<T>* col = scratch(t, static_cast<std::size_t>(Y) + fftY_.scratch_size());
-    cx<T>* fs = col + Y;
-    for (i64 task = b; task < e; ++task) {
-      const int c = static_cast<int>(task / L), zl = static_cast<int>(task % L);
-      std::fill(col, col + Y, mk<T>(T(0), T(0)));
-      for (int k = p.colOffsets[c]; k < p.colOffsets[c + 1]; ++k)
-        col[p.colY[k]] = cvt<T>(slab[layout_.colEntryBase[k] + zl]);
-      if (r2c && c == p.colOfX0) hermitian_fill(col, Y);
-      fftY_.execute(col, 1, inter + (static_cast<i64>(zl) * C + c) * Y, 1, +1, fs);
-    }
-  });
+  const int Y = p.dimY;
+  std::fill(a, a + Y, vzero<T>());
+  for (int k = p.colOffsets[c]; k < p.colOffsets[c + 1]; ++k) {
+    const BT* src = slab + layout_.colEntryBase[k] + z0;
+    VC& d = a[p.colY[k]];
+    if (std::is_same<BT, cx<T>>::value && nl == W)
+      d = load_aos<T>(reinterpret_cast<const cx<T>*>(src));
+    else
+      for (int l = 0; l < nl; ++l) set_lane<T>(d, l, cvt<T>(src[l]));
+  }
+  if (p.type == SPFFT_TRANS_R2C && c == p.colOfX0)
+    for (int l = 0; l < nl; ++l) hermitian_lane<T>(a, Y, l);
+  fft(fftY_, a, w, nl, +1);
 }
 
+// Column c's y-lines (a[0..Y), forward-transformed in place) -> slab side.
 template <typename T>
-void HostExecutor<T>::x_backward(const cx<T>* inter, T* space) {
+template <typename BT>
+void HostExecutor<T>::y_col_forward(VC* a, int c, int z0, int nl, BT* slab, VC* w) {
+  const IndexPlan& p = *plan_;
+  fft(fftY_, a, w, nl, -1);
+  for (int k = p.colOffsets[c]; k < p.colOffsets[c + 1]; ++k) {
+    BT* dst = slab + layout_.colEntryBase[k] + z0;
+    const VC& v = a[p.colY[k]];
+    if (std::is_same<BT, cx<T>>::value && nl == W)
+      store_aos<T>(reinterpret_cast<cx<T>*>(dst), v);
+    else
+      for (int l = 0; l < nl; ++l) dst[l] = cvt<typename BT::value_type>(lane<T>(v, l));
+  }
+}
+
+// nl space rows (row l starts at rows[l]) from their column values col(c)
+// (batch elements, lanes = rows): x-FFT C2C, packed-real C2R, or complex C2R.
+// a: X+1 elements, w: 2X+1 elements of scratch.
+template <typename T>
+template <class Col>
+void HostExecutor<T>::x_rows_backward(Col col, int nl, T* const* rows, VC* a, VC* w) {
+  const IndexPlan& p = *plan_;
+  const int X = p.dimX, C = p.num_columns();
+  const int n = fftX_.size();
+  VC* xv = packedReal_ ? w + X : a;  // X[x] for x in [0, dimXFreq)
+  std::fill(xv, xv + (packedReal_ ? n + 1 : X), vzero<T>());
+  for (int c = 0; c < C; ++c) xv[p.colX[c]] = col(c);
+  if (p.type != SPFFT_TRANS_R2C) {
+    fft(fftX_, a, w, nl, +1);
+    for (int l = 0; l < nl; ++l) {
+      cx<T>* out = reinterpret_cast<cx<T>*>(rows[l]);
+      for (int x = 0; x < X; ++x) out[x] = lane<T>(a[x], l);
+    }
+  } else if (packedReal_) {
+    // C2R as a half-length complex FFT: Z[k] = (X[k] + conj X[h-k]) +
+    // i (X[k] - conj X[h-k]) w^k, w = exp(+2 pi i / X); imaginary parts of
+    // X[0] and X[h] ignored; row = interleave(Re, Im) of IDFT_h(Z)
+    const int h = n;
+    for (int k = 0; k < h; ++k) {
+      VC xk = xv[k], xm = xv[h - k];
+      if (k == 0) {
+        xk.y = V(T(0));
+        xm.y = V(T(0));
+      }
+      VC xmc = xm;
+      xmc.y = -xm.y;
+      const VC sm = xk + xmc, d = xk - xmc;
+      const VC dw = twv<+1>(d, twX_[k]);  // d * exp(+2 pi i k / X)
+      VC z;
+      z.x = sm.x - dw.y;
+      z.y = sm.y + dw.x;
+      a[k] = z;
+    }
+    fft(fftX_, a, w, nl, +1);
+    for (int l = 0; l < nl; ++l) {
+      cx<T>* out = reinterpret_cast<cx<T>*>(rows[l]);  // (x[2m], x[2m+1]) pairs
+      for (int m = 0; m < h; ++m) out[m] = lane<T>(a[m], l);
+    }
+  } else {
+    for (int x = p.dimXFreq; x < X; ++x) {
+      a[x] = a[X - x];
+      a[x].y = -a[x].y;
+    }
+    fft(fftX_, a, w, nl, +1);
+    for (int l = 0; l < nl; ++l)
+      for (int x = 0; x < X; ++x) rows[l][x] = lane<T>(a[x], l).x;
+  }
+}
+
+// nl space rows -> column values put(c, batch element) (lanes = rows).
+template <typename T>
+template <class Put>
+void HostExecutor<T>::x_rows_forward(const T* const* rows, int nl, Put put, VC* a, VC* w) {
+  const IndexPlan& p = *plan_;
+  const int X = p.dimX, C = p.num_columns();
+  const int n = fftX_.size();
+  if (nl < W) std::fill(a, a + n + 1, vzero<T>());
+  if (p.type != SPFFT_TRANS_R2C) {
+    for (int l = 0; l < nl; ++l) {
+      const cx<T>* in = reinterpret_cast<const cx<T>*>(rows[l]);
+      for (int x = 0; x < X; ++x) set_lane<T>(a[x], l, in[x]);
+    }
+    fft(fftX_, a, w, nl, -1);
+    for (int c = 0; c < C; ++c) put(c, a[p.colX[c]]);
+  } else if (packedReal_) {
+    // R2C as a half-length complex FFT of y[m] = x[2m] + i x[2m+1]:
+    // X[k] = (Y[k] + conj Y[h-k]) / 2 + w^k (Y[k] - conj Y[h-k]) / (2i),
+    // w = exp(-2 pi i / X), Y[h] = Y[0]
+    const int h = n;
+    for (int l = 0; l < nl; ++l) {
+      const cx<T>* in = reinterpret_cast<const cx<T>*>(rows[l]);
+      for (int m = 0; m < h; ++m) set_lane<T>(a[m], l, in[m]);
+    }
+    fft(fftX_, a, w, nl, -1);
+    for (int c = 0; c < C; ++c) {
+      const int k = p.colX[c];
+      const VC yk = a[k == h ? 0 : k];
+      VC ym = a[k == 0 ? 0 : h - k];
+      ym.y = -ym.y;
+      VC ev = yk + ym;
+      ev.x *= T(0.5);
+      ev.y *= T(0.5);
+      const VC dd = yk - ym;
+      VC o;  // (yk - ym) / (2i)
+      o.x = dd.y * T(0.5);
+      o.y = -dd.x * T(0.5);
+      put(c, ev + twv<-1>(o, twX_[k]));
+    }
+  } else {
+    for (int l = 0; l < nl; ++l)
+      for (int x = 0; x < X; ++x) set_lane<T>(a[x], l, mk<T>(rows[l][x], T(0)));
+    fft(fftX_, a, w, nl, -1);
+    for (int c = 0; c < C; ++c) put(c, a[p.colX[c]]);
+  }
+}
+
+// Fused y/x stages (fuseXY_): a task is a block of W planes; its y-lines of
+// every column are transformed into a cache-resident plane-block buffer
+// (columns x y, lanes = planes) and the x-lines of every row read it from
+// there, so the intermediate never goes to memory (the host's DRAM bandwidth
+// per core, not the FFT arithmetic, bounds the separate stages).
+template <typename T>
+std::size_t HostExecutor<T>::block_scratch() const {
+  const IndexPlan& p = *plan_;
+  const std::size_t X = p.dimX, Y = p.dimY, Z = p.dimZ;
+  const std::size_t line = std::max({X, Y, Z});
+  return (fuseXY_ ? static_cast<std::size_t>(p.num_columns()) * block_stride() : 0) + 4 * line + 8;
+}
+
+// ---------------------------------------------------------------- backward
+template <typename T>
+template <typename BT>
+void HostExecutor<T>::yx_backward(const BT* slab, cx<T>* inter, T* space) {
   const IndexPlan& p = *plan_;
   const int X = p.dimX, Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   const bool r2c = p.type == SPFFT_TRANS_R2C;
-  grid_->pool().parallel_for(static_cast<i64>(L) * Y, 16, [&](i64 b, i64 e, int t) {
-    cx<T>* row = scratch(t, static_cast<std::size_t>(X) + fftX_.scratch_size());
-    cx<T>* fs = row + X;
-    for (i64 rIdx = b; rIdx < e; ++rIdx) {
-      const i64 zl = rIdx / Y, y = rIdx % Y;
-      std::fill(row, row + X, mk<T>(T(0), T(0)));
-      for (int c = 0; c < C; ++c) row[p.colX[c]] = inter[(zl * C + c) * Y + y];
-      if (!r2c) {
-        fftX_.execute(row, 1, reinterpret_cast<cx<T>*>(space) + rIdx * X, 1, +1, fs);
-      } else {
-        for (int x = p.dimXFreq; x < X; ++x) row[x] = conj(row[X - x]);
-        fftX_.execute(row, 1, row, 1, +1, fs);
-        T* out = space + rIdx * X;
-        for (int x = 0; x < X; ++x) out[x] = row[x].x;
+  const i64 nb = (L + W - 1) / W;
+  auto row = [&](i64 z, i64 y) -> T* {
+    return r2c ? space + (z * Y + y) * X : reinterpret_cast<T*>(reinterpret_cast<cx<T>*>(space) + (z * Y + y) * X);
+  };
+  if (fuseXY_) {
+    SPFFT_TIMED_SCOPE("yx_fft");
+    grid_->pool().parallel_for(nb, 1, [&](i64 b, i64 e, int t) {
+      VC* P = scratch(t, block_scratch());
+      const i64 ps = block_stride();
+      VC* a = P + static_cast<std::size_t>(C) * ps;
+      VC* w = a + X + 1;
+      for (i64 zb = b; zb < e; ++zb) {
+        const int z0 = static_cast<int>(zb) * W;
+        const int nl = std::min(W, L - z0);
+        for (int c = 0; c < C; ++c) y_col_backward(slab, c, z0, nl, P + c * ps, w);
+        T* rows[W];
+        for (int y = 0; y < Y; ++y) {
+          for (int l = 0; l < nl; ++l) rows[l] = row(z0 + l, y);
+          x_rows_backward([&](int c) { return P[c * ps + y]; }, nl, rows, a, w);
+        }
       }
+    });
+    return;
+  }
+  {
+    SPFFT_TIMED_SCOPE("y_fft");
+    grid_->pool().parallel_for(C * nb, 4, [&](i64 b, i64 e, int t) {
+      VC* a = scratch(t, block_scratch());
+      VC* w = a + Y;
+      for (i64 task = b; task < e; ++task) {
+        const int c = static_cast<int>(task / nb);
+        const int z0 = static_cast<int>(task % nb) * W;
+        const int nl = std::min(W, L - z0);
+        y_col_backward(slab, c, z0, nl, a, w);
+        for (int l = 0; l < nl; ++l) {
+          cx<T>* out = inter + (static_cast<i64>(z0 + l) * C + c) * Y;
+          for (int y = 0; y < Y; ++y) out[y] = lane<T>(a[y], l);
+        }
+      }
+    });
+  }
+  SPFFT_TIMED_SCOPE("x_fft");
+  // task = (plane, block of W consecutive rows): a column's W values are
+  // contiguous in the [z][column][y] intermediate
+  const i64 yb = (Y + W - 1) / W;
+  grid_->pool().parallel_for(static_cast<i64>(L) * yb, 4, [&](i64 b, i64 e, int t) {
+    VC* a = scratch(t, block_scratch());
+    VC* w = a + X + 1;
+    for (i64 task = b; task < e; ++task) {
+      const i64 zl = task / yb;
+      const int y0 = static_cast<int>(task % yb) * W;
+      const int nl = std::min(W, Y - y0);
+      T* rows[W];
+      for (int l = 0; l < nl; ++l) rows[l] = row(zl, y0 + l);
+      x_rows_backward([&](int c) {
+        const cx<T>* src = inter + (zl * C + c) * Y + y0;
+        if (nl == W) return load_aos<T>(src);
+        VC v = vzero<T>();
+        for (int l = 0; l < nl; ++l) set_lane<T>(v, l, src[l]);
+        return v;
+      }, nl, rows, a, w);
     }
   });
 }
 
 // ----------------------------------------------------------------- forward
 template <typename T>
-void HostExecutor<T>::x_forward(const T* space, cx<T>* inter) {
+template <typename BT>
+void HostExecutor<T>::xy_forward(const T* space, cx<T>* inter, BT* slab) {
   const IndexPlan& p = *plan_;
   const int X = p.dimX, Y = p.dimY, L = p.local_planes(), C = p.num_columns();
   const bool r2c = p.type == SPFFT_TRANS_R2C;
-  grid_->pool().parallel_for(static_cast<i64>(L) * Y, 16, [&](i64 b, i64 e, int t) {
-    cx<T>* row = scratch(t, static_cast<std::size_t>(X) + fftX_.scratch_size());
-    cx<T>* fs = row + X;
-    for (i64 rIdx = b; rIdx < e; ++rIdx) {
-      const i64 zl = rIdx / Y, y = rIdx % Y;
-      if (!r2c) {
-        fftX_.execute(reinterpret_cast<const cx<T>*>(space) + rIdx * X, 1, row, 1, -1, fs);
-      } else {
-        const T* in = space + rIdx * X;
-        for (int x = 0; x < X; ++x) row[x] = mk<T>(in[x], T(0));
-        fftX_.execute(row, 1, row, 1, -1, fs);
+  const i64 nb = (L + W - 1) / W;
+  auto row = [&](i64 z, i64 y) -> const T* {
+    return r2c ? space + (z * Y + y) * X
+               : reinterpret_cast<const T*>(reinterpret_cast<const cx<T>*>(space) + (z * Y + y) * X);
+  };
+  if (fuseXY_) {
+    SPFFT_TIMED_SCOPE("xy_fft");
+    grid_->pool().parallel_for(nb, 1, [&](i64 b, i64 e, int t) {
+      VC* P = scratch(t, block_scratch());
+      const i64 ps = block_stride();
+      VC* a = P + static_cast<std::size_t>(C) * ps;
+      VC* w = a + X + 1;
+      for (i64 zb = b; zb < e; ++zb) {
+        const int z0 = static_cast<int>(zb) * W;
+        const int nl = std::min(W, L - z0);
+        const T* rows[W];
+        for (int y = 0; y < Y; ++y) {
+          for (int l = 0; l < nl; ++l) rows[l] = row(z0 + l, y);
+          x_rows_forward(rows, nl, [&](int c, const VC& v) { P[c * ps + y] = v; }, a, w);
+        }
+        for (int c = 0; c < C; ++c) y_col_forward(P + c * ps, c, z0, nl, slab, w);
       }
-      for (int c = 0; c < C; ++c) inter[(zl * C + c) * Y + y] = row[p.colX[c]];
-    }
-  });
-}
-
-template <typename T>
-template <typename BT>
-void HostExecutor<T>::y_forward(const cx<T>* inter, BT* slab) {
-  const IndexPlan& p = *plan_;
-  const int Y = p.dimY, L = p.local_planes(), C = p.num_columns();
-  grid_->pool().parallel_for(static_cast<i64>(C) * L, std::max(1, L / 4), [&](i64 b, i64 e, int t) {
-    cx<T>* col = scratch(t, static_cast<std::size_t>(Y) + fftY_.scratch_size());
-    cx<T>* fs = col + Y;
+    });
+    return;
+  }
+  {
+    SPFFT_TIMED_SCOPE("x_fft");
+    const i64 yb = (Y + W - 1) / W;
+    grid_->pool().parallel_for(static_cast<i64>(L) * yb, 4, [&](i64 b, i64 e, int t) {
+      VC* a = scratch(t, block_scratch());
+      VC* w = a + X + 1;
+      for (i64 task = b; task < e; ++task) {
+        const i64 zl = task / yb;
+        const int y0 = static_cast<int>(task % yb) * W;
+        const int nl = std::min(W, Y - y0);
+        const T* rows[W];
+        for (int l = 0; l < nl; ++l) rows[l] = row(zl, y0 + l);
+        x_rows_forward(rows, nl, [&](int c, const VC& v) {
+          cx<T>* dst = inter + (zl * C + c) * Y + y0;
+          if (nl == W)
+            store_aos<T>(dst, v);
+          else
+            for (int l = 0; l < nl; ++l) dst[l] = lane<T>(v, l);
+        }, a, w);
+      }
+    });
+  }
+  SPFFT_TIMED_SCOPE("y_fft");
+  grid_->pool().parallel_for(C * nb, 4, [&](i64 b, i64 e, int t) {
+    VC* a = scratch(t, block_scratch());
+    VC* w = a + Y;
     for (i64 task = b; task < e; ++task) {
-      const int c = static_cast<int>(task / L), zl = static_cast<int>(task % L);
-      fftY_.execute(inter + (static_cast<i64>(zl) * C + c) * Y, 1, col, 1, -1, fs);
-      for (int k = p.colOffsets[c]; k < p.colOffsets[c + 1]; ++k)
-        slab[layout_.colEntryBase[k] + zl] = cvt<typename BT::value_type>(col[p.colY[k]]);
+      const int c = static_cast<int>(task / nb);
+      const int z0 = static_cast<int>(task % nb) * W;
+      const int nl = std::min(W, L - z0);
+      if (nl < W) std::fill(a, a + Y, vzero<T>());
+      for (int l = 0; l < nl; ++l) {
+        const cx<T>* in = inter + (static_cast<i64>(z0 + l) * C + c) * Y;
+        for (int y = 0; y < Y; ++y) set_lane<T>(a[y], l, in[y]);
+      }
+      y_col_forward(a, c, z0, nl, slab, w);
     }
   });
 }
@@ -169,21 +430,33 @@ void HostExecutor<T>::y_forward(const cx<T>* inter, BT* slab) {
 template <typename T>
 template <typename BT>
 void HostExecutor<T>::z_forward(const BT* stick, cx<T>* values, T factor) {
+  SPFFT_TIMED_SCOPE("z_fft");
   const IndexPlan& p = *plan_;
   const int Z = p.dimZ;
-  grid_->pool().parallel_for(p.local_sticks(), 16, [&](i64 b, i64 e, int t) {
-    cx<T>* buf = scratch(t, static_cast<std::size_t>(Z) + fftZ_.scratch_size());
-    cx<T>* fs = buf + Z;
-    for (i64 s = b; s < e; ++s) {
-      for (int r = 0; r < p.size; ++r) {
-        const BT* src = stick + layout_.stickDispl[r] + s * layout_.stickStride[r];
-        cx<T>* dst = buf + p.planeOffsets[r];
-        for (int z = 0; z < p.planesPerRank[r]; ++z) dst[z] = cvt<T>(src[z]);
+  const i64 S = p.local_sticks();
+  grid_->pool().parallel_for((S + W - 1) / W, 4, [&](i64 b, i64 e, int t) {
+    VC* a = scratch(t, block_scratch());
+    VC* w = a + Z;
+    for (i64 blk = b; blk < e; ++blk) {
+      const i64 s0 = blk * W;
+      const int nl = static_cast<int>(std::min<i64>(W, S - s0));
+      if (nl < W) std::fill(a, a + Z, vzero<T>());
+      for (int l = 0; l < nl; ++l) {
+        const i64 s = s0 + l;
+        for (int r = 0; r < p.size; ++r) {
+          const BT* src = stick + layout_.stickDispl[r] + s * layout_.stickStride[r];
+          VC* dst = a + p.planeOffsets[r];
+          for (int z = 0; z < p.planesPerRank[r]; ++z) set_lane<T>(dst[z], l, cvt<T>(src[z]));
+        }
       }
-      fftZ_.execute(buf, 1, buf, 1, -1, fs);
-      for (int q = p.stickRunOffsets[s]; q < p.stickRunOffsets[s + 1]; ++q) {
-        const StickRun& r = p.runs[q];
-        for (int j = 0; j < r.length; ++j) values[r.valueStart + j] = scale(buf[r.zStart + j], factor);
+      fft(fftZ_, a, w, nl, -1);
+      for (int l = 0; l < nl; ++l) {
+        const i64 s = s0 + l;
+        for (int q = p.stickRunOffsets[s]; q < p.stickRunOffsets[s + 1]; ++q) {
+          const StickRun& r = p.runs[q];
+          for (int j = 0; j < r.length; ++j)
+            values[r.valueStart + j] = scale(lane<T>(a[r.zStart + j], l), factor);
+        }
       }
     }
   });
@@ -255,10 +528,9 @@ void HostExecutor<T>::backward_xy() {
   void* slab = grid_->host_slot(dist ? GridImpl<T>::kSlabSide : GridImpl<T>::kStickSide);
   auto* inter = static_cast<cx<T>*>(grid_->host_slot(GridImpl<T>::kInter));
   if (floatExchange_)
-    y_backward(static_cast<const cx<float>*>(slab), inter);
+    yx_backward(static_cast<const cx<float>*>(slab), inter, space_domain());
   else
-    y_backward(static_cast<const cx<T>*>(slab), inter);
-  x_backward(inter, space_domain());
+    yx_backward(static_cast<const cx<T>*>(slab), inter, space_domain());
 }
 
 template <typename T>
@@ -267,12 +539,11 @@ void HostExecutor<T>::forward_xy() {
   poison(false);
   const bool dist = plan_->size > 1;
   auto* inter = static_cast<cx<T>*>(grid_->host_slot(GridImpl<T>::kInter));
-  x_forward(space_domain(), inter);
   void* slab = grid_->host_slot(dist ? GridImpl<T>::kSlabSide : GridImpl<T>::kStickSide);
   if (floatExchange_)
-    y_forward(inter, static_cast<cx<float>*>(slab));
+    xy_forward(space_domain(), inter, static_cast<cx<float>*>(slab));
   else
-    y_forward(inter, static_cast<cx<T>*>(slab));
+    xy_forward(space_domain(), inter, static_cast<cx<T>*>(slab));
 }
 
 template <typename T>

@@ -9,7 +9,7 @@
 #include <vector>
 
 #include "api/grid_impl.hpp"
-#include "fft/host_fft.hpp"
+#include "fft/host_fft_batch.hpp"
 #include "plan/index_plan.hpp"
 
 namespace spfft {
@@ -30,26 +30,44 @@ public:
   T* space_domain() { return static_cast<T*>(grid_->host_slot(GridImpl<T>::kSpace)); }
 
 private:
+  using Fft = HostFftBatch<T>;
+  using VC = typename HostSimd<T>::VC;
+  using V = typename HostSimd<T>::V;
+  static constexpr int W = HostSimd<T>::W;
+  void fft(const Fft& f, VC* a, VC* b, int nl, int sign);
   template <typename BT>
   void z_backward(const cx<T>* values, BT* stickSide);
   template <typename BT>
-  void y_backward(const BT* slabSide, cx<T>* inter);
-  template <typename BT>
-  void y_forward(const cx<T>* inter, BT* slabSide);
-  template <typename BT>
   void z_forward(const BT* stickSide, cx<T>* values, T scale);
-  void x_backward(const cx<T>* inter, T* space);
-  void x_forward(const T* space, cx<T>* inter);
+  template <typename BT>
+  void yx_backward(const BT* slabSide, cx<T>* inter, T* space);
+  template <typename BT>
+  void xy_forward(const T* space, cx<T>* inter, BT* slabSide);
+  template <typename BT>
+  void y_col_backward(const BT* slab, int c, int z0, int nl, VC* a, VC* w);
+  template <typename BT>
+  void y_col_forward(VC* a, int c, int z0, int nl, BT* slab, VC* w);
+  template <class Col>
+  void x_rows_backward(Col col, int nl, T* const* rows, VC* a, VC* w);
+  template <class Put>
+  void x_rows_forward(const T* const* rows, int nl, Put put, VC* a, VC* w);
+  std::size_t block_scratch() const;
+  // column stride of the fused plane-block buffer: dimY + 1 elements, so the
+  // x-line gathers (one element per column) do not all hit one cache set
+  i64 block_stride() const { return plan_->dimY + 1; }
   void exchange(bool backward);
   void poison(bool backward);
-  cx<T>* scratch(int thread, std::size_t n);
+  VC* scratch(int thread, std::size_t n);
 
   std::shared_ptr<GridImpl<T>> grid_;
   std::shared_ptr<const IndexPlan> plan_;
   ExchangeLayout layout_;
   bool floatExchange_ = false;
-  HostFft<T> fftX_, fftY_, fftZ_;
-  std::vector<std::vector<cx<T>>> scratch_;
+  bool packedReal_ = false;  // R2C with even dimX: half-length x FFTs
+  bool fuseXY_ = false;      // y/x stages fused per block of W planes
+  Fft fftX_, fftY_, fftZ_;
+  std::vector<cx<T>> twX_;   // exp(-2 pi i m / dimX)
+  std::vector<std::vector<VC>> scratch_;
 };
 
 }  // namespace spfft

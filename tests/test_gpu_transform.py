@@ -920,3 +920,67 @@ def test_rccl_abort_is_reported(gpu, monkeypatch):
 
     for msgs in run_ranks(2, body):
         assert all(m is not None and "abort" in m for m in msgs), msgs
+
+
+@pytest.mark.parametrize("ttype", ["c2c", "r2c"])
+@pytest.mark.parametrize("single", [False, True])
+def test_capped_intermediate(gpu, ttype, single, monkeypatch):
+    """SPFFT_INTER_BYTES caps the grid's [z][column][y] intermediate (large-grid
+    memory mode): the y/x stages run over plane ranges that reuse it. 5 planes of
+    room for a 21-plane slab: ranges of 5, 5, 5, 5, 1 planes."""
+    import torch
+    dims = (24, 20, 21)
+    nx, ny, nz = dims
+    esize = 8 if single else 16
+    monkeypatch.setenv("SPFFT_INTER_BYTES", str(5 * nx * (ny + 8) * esize))
+    rng = np.random.default_rng(77)
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.8, 0.8, nx, ny, nz, r2c)[0]
+    G = sp.GridFloat if single else sp.Grid
+    grid = G(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    tol = 1e-4 if single else 1e-11
+    cdt = torch.complex64 if single else torch.complex128
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    rdt = torch.float32 if single else torch.float64
+    f = t.forward(torch.as_tensor(space, device=gpu, dtype=rdt if r2c else cdt))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims, r2c=r2c)) < tol
+    b = t.backward(f)
+    ref = dense_backward(idx, f.cpu().numpy().astype(np.complex128), dims, r2c=r2c)
+    assert max_rel_error(b.cpu().numpy(), ref) < tol
+
+
+@pytest.mark.parametrize("exchange,chunks", [("COMPACT_BUFFERED", 1), ("COMPACT_BUFFERED", 2),
+                                             ("BUFFERED", 2), ("UNBUFFERED", 1)])
+def test_capped_intermediate_distributed(gpu, exchange, chunks, monkeypatch):
+    """Capped intermediate on 3 virtual ranks, inside the pipelined exchange chunks."""
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    dims = (24, 20, 30)
+    nx, ny, nz = dims
+    monkeypatch.setenv("SPFFT_INTER_BYTES", str(3 * nx * (ny + 8) * 16))
+    gidx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(78)
+    vals = _rand_vals(rng, len(gidx))
+    ref = dense_backward(gidx, vals, dims)
+    P = 3
+    parts = distribute_sticks(gidx, P, dims)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU,
+                             exchange_type=getattr(sp.ExchangeType, exchange))
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.as_tensor(vals[start:start + len(s.indices)], device="cuda")
+        out = s.transform.backward(v).cpu().numpy()
+        e1 = max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length])
+        f = s.transform.forward(None, scaling=sp.Scaling.FULL).cpu().numpy()
+        return max(e1, max_rel_error(f, v.cpu().numpy()))
+
+    for e in run_ranks(P, body):
+        assert e < 1e-11

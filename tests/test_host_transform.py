@@ -129,3 +129,36 @@ def test_reference_size_sweep_full():
         if max(errs) > 1e-11:
             failures.append((dims, centered, errs))
     assert not failures, failures[:5]
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("ttype", ["c2c", "r2c"])
+@pytest.mark.parametrize("dims", [(24, 20, 17), (67, 9, 10), (15, 67, 12), (9, 10, 131),
+                                  (33, 18, 26), (8, 8, 9)])
+@pytest.mark.parametrize("single", [False, True])
+def test_batched_engine_paths(dims, ttype, fuse, single, monkeypatch):
+    """The batched SIMD host engine: fused plane-block y/x path and separate
+    stages (SPFFT_HOST_FUSE), packed-real (even dimX) and complex (odd dimX)
+    C2R/R2C x lines, partial batches (plane / row / stick counts that are not a
+    multiple of the SIMD width), Bluestein lengths (67, 131) run line by line."""
+    monkeypatch.setenv("SPFFT_HOST_FUSE", fuse)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    rng = np.random.default_rng(5)
+    idx = create_value_indices(rng, [1.0], 0.8, 0.8, nx, ny, nz, r2c)[0]
+    G = sp.GridFloat if single else sp.Grid
+    grid = G(nx, ny, nz, nx * ny, HOST, 3)
+    t = grid.create_transform(HOST, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    tol = 2e-4 if single else 1e-11
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    space = space.astype((np.float32 if r2c else np.complex64) if single else
+                         (np.float64 if r2c else np.complex128))
+    f = t.forward(space)
+    assert max_rel_error(f, dense_forward(space.astype(np.complex128 if not r2c else np.float64),
+                                          idx, dims, r2c=r2c)) < tol
+    b = t.backward(f)
+    ref = dense_backward(idx, np.asarray(f).astype(np.complex128), dims, r2c=r2c)
+    assert max_rel_error(b, ref) < tol
