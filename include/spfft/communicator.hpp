@@ -21,6 +21,14 @@
 
 namespace spfft {
 
+/* A started host exchange: wait() completes it. The send and receive buffers
+ * stay in use until then. */
+class SPFFT_EXPORT ExchangeRequest {
+public:
+  virtual ~ExchangeRequest();
+  virtual void wait() = 0;
+};
+
 class SPFFT_EXPORT Communicator {
 public:
   virtual ~Communicator();
@@ -35,6 +43,15 @@ public:
   virtual void alltoallv(const void* send, const std::size_t* sendCounts,
                          const std::size_t* sendDispls, void* recv, const std::size_t* recvCounts,
                          const std::size_t* recvDispls) = 0;
+
+  /* Non-blocking alltoallv (the reference's MPI_Ialltoallv exchanges,
+   * src/transpose/transpose_mpi_compact_buffered_host.cpp:189,274). The count
+   * and displacement arrays may be released on return. The default runs
+   * alltoallv() at once and returns a completed request. */
+  virtual std::unique_ptr<ExchangeRequest> ialltoallv(const void* send, const std::size_t* sendCounts,
+                                                      const std::size_t* sendDispls, void* recv,
+                                                      const std::size_t* recvCounts,
+                                                      const std::size_t* recvDispls);
 
   virtual void barrier();
 

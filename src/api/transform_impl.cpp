@@ -112,7 +112,7 @@ void TransformImpl<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
 template <typename T>
 void TransformImpl<T>::forward_exchange(bool nonBlocking) {
   if (host_)
-    host_->forward_exchange();
+    host_->forward_exchange(nonBlocking);
   else
     gpu_->forward_exchange(nonBlocking);
 }
@@ -137,7 +137,7 @@ void TransformImpl<T>::backward_z(const T* input) {
 template <typename T>
 void TransformImpl<T>::backward_exchange(bool nonBlocking) {
   if (host_)
-    host_->backward_exchange();
+    host_->backward_exchange(nonBlocking);
   else
     gpu_->backward_exchange(nonBlocking);
 }

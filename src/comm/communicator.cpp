@@ -9,6 +9,21 @@
 namespace spfft {
 
 Communicator::~Communicator() = default;
+ExchangeRequest::~ExchangeRequest() = default;
+
+namespace {
+struct CompletedRequest : ExchangeRequest {
+  void wait() override {}
+};
+}  // namespace
+
+std::unique_ptr<ExchangeRequest> Communicator::ialltoallv(const void* send, const std::size_t* sc,
+                                                          const std::size_t* sd, void* recv,
+                                                          const std::size_t* rc,
+                                                          const std::size_t* rd) {
+  alltoallv(send, sc, sd, recv, rc, rd);
+  return std::unique_ptr<ExchangeRequest>(new CompletedRequest());
+}
 
 void Communicator::barrier() {
   char token = 0;

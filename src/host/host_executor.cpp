@@ -482,6 +482,7 @@ void HostExecutor<T>::poison(bool backward) {
 template <typename T>
 void HostExecutor<T>::backward_z(const T* input) {
   SPFFT_TIMED_SCOPE("backward_z");
+  finish_exchange();
   poison(true);
   void* stick = grid_->host_slot(GridImpl<T>::kStickSide);
   const auto* values = reinterpret_cast<const cx<T>*>(input);
@@ -493,7 +494,16 @@ void HostExecutor<T>::backward_z(const T* input) {
 }
 
 template <typename T>
-void HostExecutor<T>::exchange(bool backward) {
+void HostExecutor<T>::finish_exchange() {
+  if (!pending_) return;
+  SPFFT_TIMED_SCOPE("exchange_wait");
+  std::unique_ptr<ExchangeRequest> r = std::move(pending_);
+  r->wait();
+}
+
+template <typename T>
+void HostExecutor<T>::exchange(bool backward, bool nonBlocking) {
+  finish_exchange();
   if (plan_->size <= 1) return;
   const std::size_t elemBytes = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   const int P = plan_->size;
@@ -509,21 +519,24 @@ void HostExecutor<T>::exchange(bool backward) {
   }
   void* stick = grid_->host_slot(GridImpl<T>::kStickSide);
   void* slab = grid_->host_slot(GridImpl<T>::kSlabSide);
-  if (backward)
-    grid_->communicator()->alltoallv(stick, sc.data(), sd.data(), slab, rc.data(), rd.data());
+  const void* src = backward ? stick : slab;
+  void* dst = backward ? slab : stick;
+  if (nonBlocking)
+    pending_ = grid_->communicator()->ialltoallv(src, sc.data(), sd.data(), dst, rc.data(), rd.data());
   else
-    grid_->communicator()->alltoallv(slab, sc.data(), sd.data(), stick, rc.data(), rd.data());
+    grid_->communicator()->alltoallv(src, sc.data(), sd.data(), dst, rc.data(), rd.data());
 }
 
 template <typename T>
-void HostExecutor<T>::backward_exchange() {
-  SPFFT_TIMED_SCOPE("backward_exchange");
-  exchange(true);
+void HostExecutor<T>::backward_exchange(bool nonBlocking) {
+  SPFFT_TIMED_SCOPE(nonBlocking ? "backward_exchange_start" : "backward_exchange");
+  exchange(true, nonBlocking);
 }
 
 template <typename T>
 void HostExecutor<T>::backward_xy() {
   SPFFT_TIMED_SCOPE("backward_xy");
+  finish_exchange();
   const bool dist = plan_->size > 1;
   void* slab = grid_->host_slot(dist ? GridImpl<T>::kSlabSide : GridImpl<T>::kStickSide);
   auto* inter = static_cast<cx<T>*>(grid_->host_slot(GridImpl<T>::kInter));
@@ -536,6 +549,7 @@ void HostExecutor<T>::backward_xy() {
 template <typename T>
 void HostExecutor<T>::forward_xy() {
   SPFFT_TIMED_SCOPE("forward_xy");
+  finish_exchange();
   poison(false);
   const bool dist = plan_->size > 1;
   auto* inter = static_cast<cx<T>*>(grid_->host_slot(GridImpl<T>::kInter));
@@ -547,14 +561,15 @@ void HostExecutor<T>::forward_xy() {
 }
 
 template <typename T>
-void HostExecutor<T>::forward_exchange() {
-  SPFFT_TIMED_SCOPE("forward_exchange");
-  exchange(false);
+void HostExecutor<T>::forward_exchange(bool nonBlocking) {
+  SPFFT_TIMED_SCOPE(nonBlocking ? "forward_exchange_start" : "forward_exchange");
+  exchange(false, nonBlocking);
 }
 
 template <typename T>
 void HostExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   SPFFT_TIMED_SCOPE("forward_z");
+  finish_exchange();
   if (plan_->numLocalElements > 0 && !output) throw InvalidParameterError();
   const T factor =
       scaling == SPFFT_FULL_SCALING

@@ -11,6 +11,7 @@
 #include "api/grid_impl.hpp"
 #include "fft/host_fft_batch.hpp"
 #include "plan/index_plan.hpp"
+#include "spfft/communicator.hpp"
 
 namespace spfft {
 
@@ -21,10 +22,13 @@ public:
 
   // Step-wise API (reference: execution_host.hpp:70-81).
   void backward_z(const T* input);
-  void backward_exchange();
+  // nonBlocking: start the exchange and return; the next stage of the same
+  // direction (backward_xy / forward_z) completes it (reference:
+  // src/spfft/transform_internal.cpp:195-198, 277-282)
+  void backward_exchange(bool nonBlocking = false);
   void backward_xy();
   void forward_xy();
-  void forward_exchange();
+  void forward_exchange(bool nonBlocking = false);
   void forward_z(T* output, SpfftScalingType scaling);
 
   T* space_domain() { return static_cast<T*>(grid_->host_slot(GridImpl<T>::kSpace)); }
@@ -55,7 +59,9 @@ private:
   // column stride of the fused plane-block buffer: dimY + 1 elements, so the
   // x-line gathers (one element per column) do not all hit one cache set
   i64 block_stride() const { return plan_->dimY + 1; }
-  void exchange(bool backward);
+  void exchange(bool backward, bool nonBlocking);
+  void finish_exchange();
+  std::unique_ptr<ExchangeRequest> pending_;
   void poison(bool backward);
   VC* scratch(int thread, std::size_t n);
 

@@ -68,10 +68,17 @@ public:
                             MPI_BYTE, comm_));
   }
 
-  void alltoallv(const void* send, const std::size_t* sc, const std::size_t* sd, void* recv,
-                 const std::size_t* rc, const std::size_t* rd) override {
-    // counts/displacements are bytes; use the largest element unit that divides
-    // all of them so that int counts reach far beyond 2 GiB
+  // Byte counts/displacements in the largest element unit that divides all of
+  // them (16, 8, 4 or 1 bytes), so that int counts reach far beyond 2 GiB.
+  struct Counts {
+    MPI_Datatype type = MPI_DATATYPE_NULL;
+    std::vector<int> sc, sd, rc, rd;
+    ~Counts() {
+      if (type != MPI_DATATYPE_NULL && !mpi_finalized()) MPI_Type_free(&type);
+    }
+  };
+  void make_counts(Counts& c, const std::size_t* sc, const std::size_t* sd, const std::size_t* rc,
+                   const std::size_t* rd) const {
     std::size_t g = 0;
     for (int r = 0; r < size_; ++r) g = std::gcd(g, std::gcd(std::gcd(sc[r], sd[r]), std::gcd(rc[r], rd[r])));
     std::size_t unit = 1;
@@ -81,26 +88,53 @@ public:
         break;
       }
     }
-    MPI_Datatype type;
-    mpi_check(MPI_Type_contiguous(static_cast<int>(unit), MPI_BYTE, &type));
-    mpi_check(MPI_Type_commit(&type));
-    std::vector<int> isc(size_), isd(size_), irc(size_), ird(size_);
+    c.sc.resize(size_);
+    c.sd.resize(size_);
+    c.rc.resize(size_);
+    c.rd.resize(size_);
     for (int r = 0; r < size_; ++r) {
       const std::size_t v[4] = {sc[r] / unit, sd[r] / unit, rc[r] / unit, rd[r] / unit};
       for (std::size_t x : v)
-        if (x > static_cast<std::size_t>(INT_MAX)) {
-          MPI_Type_free(&type);
-          throw OverflowError();
-        }
-      isc[r] = static_cast<int>(v[0]);
-      isd[r] = static_cast<int>(v[1]);
-      irc[r] = static_cast<int>(v[2]);
-      ird[r] = static_cast<int>(v[3]);
+        if (x > static_cast<std::size_t>(INT_MAX)) throw OverflowError();
+      c.sc[r] = static_cast<int>(v[0]);
+      c.sd[r] = static_cast<int>(v[1]);
+      c.rc[r] = static_cast<int>(v[2]);
+      c.rd[r] = static_cast<int>(v[3]);
     }
-    const int st = MPI_Alltoallv(send, isc.data(), isd.data(), type, recv, irc.data(), ird.data(),
-                                 type, comm_);
-    MPI_Type_free(&type);
-    mpi_check(st);
+    mpi_check(MPI_Type_contiguous(static_cast<int>(unit), MPI_BYTE, &c.type));
+    mpi_check(MPI_Type_commit(&c.type));
+  }
+
+  void alltoallv(const void* send, const std::size_t* sc, const std::size_t* sd, void* recv,
+                 const std::size_t* rc, const std::size_t* rd) override {
+    Counts c;
+    make_counts(c, sc, sd, rc, rd);
+    mpi_check(MPI_Alltoallv(send, c.sc.data(), c.sd.data(), c.type, recv, c.rc.data(), c.rd.data(),
+                            c.type, comm_));
+  }
+
+  // MPI_Ialltoallv: the counts and the datatype live in the request until the
+  // exchange completed (the MPI standard requires them until completion)
+  struct Request : ExchangeRequest {
+    Counts counts;
+    MPI_Request req = MPI_REQUEST_NULL;
+    ~Request() override {
+      if (req != MPI_REQUEST_NULL && !mpi_finalized()) MPI_Wait(&req, MPI_STATUS_IGNORE);
+    }
+    void wait() override {
+      if (req != MPI_REQUEST_NULL) mpi_check(MPI_Wait(&req, MPI_STATUS_IGNORE));
+    }
+  };
+  std::unique_ptr<ExchangeRequest> ialltoallv(const void* send, const std::size_t* sc,
+                                              const std::size_t* sd, void* recv,
+                                              const std::size_t* rc,
+                                              const std::size_t* rd) override {
+    std::unique_ptr<Request> r(new Request());
+    make_counts(r->counts, sc, sd, rc, rd);
+    Counts& c = r->counts;
+    mpi_check(MPI_Ialltoallv(send, c.sc.data(), c.sd.data(), c.type, recv, c.rc.data(),
+                             c.rd.data(), c.type, comm_, &r->req));
+    return std::unique_ptr<ExchangeRequest>(r.release());
   }
 
   void barrier() override { mpi_check(MPI_Barrier(comm_)); }

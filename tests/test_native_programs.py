@@ -99,3 +99,22 @@ def test_bench_cli_gpu(gpu, tmp_path):
           "-p", "gpu-gpu", "--cutoff", "0.5"])
     j = json.loads(out.read_text())
     assert j["results"][0]["transforms_per_second"] > 0
+
+
+def test_host_multi_transform_nonblocking_exchange_mpi(tmp_path):
+    """Host multi_transform under mpiexec -n 2: each transform's exchange starts as an
+    MPI_Ialltoallv (backward_exchange_start / forward_exchange_start) and completes in
+    the next stage (exchange_wait), so the second transform's z / xy stage runs while
+    the first one's exchange is in flight (reference:
+    src/spfft/multi_transform_internal.hpp:61-94)."""
+    import json
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = tmp_path / "nb.json"
+    _run([MPIEXEC, "-n", "2", _prog("spfft_bench"), "-d", "32", "30", "28", "-r", "3", "-m", "2",
+          "-o", str(out), "-e", "compact", "-p", "cpu", "--cutoff", "0.5"])
+    text = out.read_text()
+    j = json.loads(text)
+    assert j["results"][0]["transforms_per_second"] > 0
+    for name in ("backward_exchange_start", "forward_exchange_start", "exchange_wait"):
+        assert name in text, name
