@@ -61,10 +61,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     const long long cap = grid_->device_slot_elements(GridImpl<T>::kInter);
     interPlanes_ = perPlane > 0 ? static_cast<int>(std::min<long long>(L, std::max(1LL, cap / perPlane))) : L;
   }
-  for (int n : {p.dimX, p.dimY, p.dimZ}) {
-    if (!dev::has_ct_kernel(n) && n > dev::max_device_fft_length(sizeof(T) == 8))
-      throw GPUFFTError();
-  }
+  setup_long_axes();
 
   ownStream_.reset(new GpuStream());
   stream_ = ownStream_->get();
@@ -92,7 +89,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(colX_, p.colX);
   upload(twX_, make_twiddles<T>(p.dimX));
   // packed-real x stage for R2C with even dimX (SPFFT_R2C_PACKED=0 disables)
-  if (p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4 &&
+  if (!longX_ && p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4 &&
       env_int("SPFFT_R2C_PACKED", 1, 0, 1) && (dev::has_ct_kernel(p.dimX / 2) ||
                                                 p.dimX / 2 <= dev::max_device_fft_length(sizeof(T) == 8)))
     upload(twXh_, make_twiddles<T>(p.dimX / 2));
@@ -161,6 +158,11 @@ void GpuExecutor<T>::log_plan() const {
   if (!env || !*env || env[0] == '0') return;
   const IndexPlan& p = *plan_;
   const bool dbl = sizeof(T) == 8;
+  auto describe = [&](bool isLong, const dev::LongPlan& lp, int n, bool lf) -> std::string {
+    if (!isLong) return dev::describe_engine(n, dbl, lf);
+    return "long n=" + std::to_string(n) + (lp.bluestein ? " bluestein m=" + std::to_string(lp.m) : "") +
+           " four-step " + std::to_string(lp.n1) + "x" + std::to_string(lp.n2);
+  };
   std::string plane = "none";
   if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
@@ -170,9 +172,8 @@ void GpuExecutor<T>::log_plan() const {
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
-               dev::describe_engine(p.dimZ, dbl, false).c_str(),
-               dev::describe_engine(p.dimY, dbl, true).c_str(),
-               dev::describe_engine(twXh_ ? p.dimX / 2 : p.dimX, dbl, true).c_str(),
+               describe(longZ_, lpZ_, p.dimZ, false).c_str(), describe(longY_, lpY_, p.dimY, true).c_str(),
+               describe(longX_, lpX_, twXh_ ? p.dimX / 2 : p.dimX, true).c_str(),
                twXh_ ? " packed-real" : "", interPlanes_, layout_.buffered ? "buffered" : "compact",
                floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, chunkModel_ / 1e6,
                peerWrites_ ? 1 : 0);
@@ -769,7 +770,13 @@ void GpuExecutor<T>::backward_z(const T* input) {
     a.segDispl = segDisplRemote_->data<long long>();
     a.remote = 1;
   }
-  if (floatExchange_)
+  if (longZ_ && floatExchange_)
+    dev::launch_long_z_backward<T, cx<float>>(lpZ_, a, values, static_cast<cx<float>*>(stick),
+                                              long_bufs(), stream_);
+  else if (longZ_)
+    dev::launch_long_z_backward<T, cx<T>>(lpZ_, a, values, static_cast<cx<T>*>(stick), long_bufs(),
+                                          stream_);
+  else if (floatExchange_)
     dev::launch_z_backward<T, cx<float>>(a, values, static_cast<cx<float>*>(stick),
                                          twZ_->data<cx<T>>(), stream_);
   else
@@ -809,6 +816,101 @@ void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   exchange(true);
 }
 
+// ------------------------------------------------------------- long axes
+// Axes longer than one workgroup's LDS (or with a large prime factor and no
+// in-LDS Bluestein) run glue kernel -> global four-step / Bluestein FFT ->
+// glue kernel instead of the fused stage kernel (kernels/long_fft.hpp).
+template <typename T>
+void GpuExecutor<T>::setup_long_axes() {
+  const IndexPlan& p = *plan_;
+  const bool dbl = sizeof(T) == 8;
+  const bool packedX = p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4;
+  const int xLen = packedX ? p.dimX / 2 : p.dimX;
+  longZ_ = dev::needs_long_path(p.dimZ, dbl);
+  longY_ = dev::needs_long_path(p.dimY, dbl);
+  longX_ = dev::needs_long_path(xLen, dbl);
+  long long elems = 0;
+  if (longZ_) {
+    lpZ_ = dev::long_plan(p.dimZ, dbl);
+    elems = std::max(elems, static_cast<long long>(p.local_sticks()) * (lpZ_.line_elems() + 2));
+  }
+  if (longY_) {
+    lpY_ = dev::long_plan(p.dimY, dbl);
+    elems = std::max(elems, static_cast<long long>(interPlanes_) * p.num_columns() *
+                                (lpY_.line_elems() + 2));
+  }
+  if (longX_) {
+    lpX_ = dev::long_plan(xLen, dbl);
+    elems = std::max(elems, static_cast<long long>(interPlanes_) * p.dimY *
+                                (std::max<long long>(lpX_.line_elems(), p.dimX) + 2));
+  }
+  if (elems == 0) return;
+  const bool blue = (longZ_ && lpZ_.bluestein) || (longY_ && lpY_.bluestein) ||
+                    (longX_ && lpX_.bluestein);
+  const std::size_t bytes = static_cast<std::size_t>(elems) * sizeof(cx<T>);
+  for (int i = 0; i < 4; ++i)
+    if (blue || i == 0 || i == 3) longWork_[i].reset(new DeviceBuffer(bytes));
+}
+
+template <typename T>
+dev::LongBufs<T> GpuExecutor<T>::long_bufs() const {
+  auto ptr = [&](int i) { return longWork_[i] ? longWork_[i]->template data<cx<T>>() : nullptr; };
+  return dev::LongBufs<T>{ptr(0), ptr(1), ptr(2), ptr(3)};
+}
+
+template <typename T>
+void GpuExecutor<T>::y_backward_launch(const dev::YArgs& ya, const void* slab, cx<T>* inter) {
+  if (longY_ && floatExchange_)
+    dev::launch_long_y_backward<T, cx<float>>(lpY_, ya, static_cast<const cx<float>*>(slab), inter,
+                                              long_bufs(), stream_);
+  else if (longY_)
+    dev::launch_long_y_backward<T, cx<T>>(lpY_, ya, static_cast<const cx<T>*>(slab), inter,
+                                          long_bufs(), stream_);
+  else if (floatExchange_)
+    dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), inter,
+                                         twY_->data<cx<T>>(), stream_);
+  else
+    dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), inter, twY_->data<cx<T>>(),
+                                     stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::y_forward_launch(const dev::YArgs& ya, cx<T>* inter, void* slab) {
+  if (longY_ && floatExchange_)
+    dev::launch_long_y_forward<T, cx<float>>(lpY_, ya, inter, static_cast<cx<float>*>(slab),
+                                             long_bufs(), stream_);
+  else if (longY_)
+    dev::launch_long_y_forward<T, cx<T>>(lpY_, ya, inter, static_cast<cx<T>*>(slab), long_bufs(),
+                                         stream_);
+  else if (floatExchange_)
+    dev::launch_y_forward<T, cx<float>>(ya, inter, static_cast<cx<float>*>(slab), twY_->data<cx<T>>(),
+                                        stream_);
+  else
+    dev::launch_y_forward<T, cx<T>>(ya, inter, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(), stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::x_backward_launch(const dev::XArgs& xa, const cx<T>* inter, void* space) {
+  const bool r2c = plan_->type == SPFFT_TRANS_R2C;
+  if (longX_)
+    dev::launch_long_x_backward<T>(lpX_, xa, r2c, inter, space, twX_->data<cx<T>>(), long_bufs(),
+                                   stream_);
+  else
+    dev::launch_x_backward<T>(xa, r2c, inter, space, twX_->data<cx<T>>(),
+                              twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::x_forward_launch(const dev::XArgs& xa, const void* space, cx<T>* inter) {
+  const bool r2c = plan_->type == SPFFT_TRANS_R2C;
+  if (longX_)
+    dev::launch_long_x_forward<T>(lpX_, xa, r2c, space, inter, twX_->data<cx<T>>(), long_bufs(),
+                                  stream_);
+  else
+    dev::launch_x_forward<T>(xa, r2c, space, inter, twX_->data<cx<T>>(),
+                             twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+}
+
 // The intermediate as seen by the y/x kernels of a plane range starting at z0:
 // they address plane z at z * interZStride, so a capped buffer is shifted to
 // hold planes [z0, z0 + interPlanes_).
@@ -846,14 +948,8 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
         set_col_desc(ya, colDescChunk_[k]);
       }
       cx<T>* in = inter_for(inter, z0);
-      if (floatExchange_)
-        dev::launch_y_backward<T, cx<float>>(ya, static_cast<const cx<float>*>(slab), in,
-                                             twY_->data<cx<T>>(), stream_);
-      else
-        dev::launch_y_backward<T, cx<T>>(ya, static_cast<const cx<T>*>(slab), in,
-                                         twY_->data<cx<T>>(), stream_);
-      dev::launch_x_backward<T>(xa, plan_->type == SPFFT_TRANS_R2C, in, space, twX_->data<cx<T>>(),
-                                twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
+      y_backward_launch(ya, slab, in);
+      x_backward_launch(xa, in, space);
     }
   }
   if (outputLocation == SPFFT_PU_HOST) {
@@ -904,14 +1000,8 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
         ya.remote = 1;
       }
       cx<T>* out = inter_for(inter, z0);
-      dev::launch_x_forward<T>(xa, plan_->type == SPFFT_TRANS_R2C, space, out, twX_->data<cx<T>>(),
-                               twXh_ ? twXh_->data<cx<T>>() : nullptr, stream_);
-      if (floatExchange_)
-        dev::launch_y_forward<T, cx<float>>(ya, out, static_cast<cx<float>*>(slab),
-                                            twY_->data<cx<T>>(), stream_);
-      else
-        dev::launch_y_forward<T, cx<T>>(ya, out, static_cast<cx<T>*>(slab), twY_->data<cx<T>>(),
-                                        stream_);
+      x_forward_launch(xa, space, out);
+      y_forward_launch(ya, out, slab);
     }
     if (K > 1) chunkEvents_[k]->record(stream_);
   }
@@ -951,7 +1041,13 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kStickSide);
   const auto a = zargs();
-  if (floatExchange_)
+  if (longZ_ && floatExchange_)
+    dev::launch_long_z_forward<T, cx<float>>(lpZ_, a, static_cast<const cx<float>*>(stick), values,
+                                             factor, long_bufs(), stream_);
+  else if (longZ_)
+    dev::launch_long_z_forward<T, cx<T>>(lpZ_, a, static_cast<const cx<T>*>(stick), values, factor,
+                                         long_bufs(), stream_);
+  else if (floatExchange_)
     dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,
                                         twZ_->data<cx<T>>(), stream_);
   else
@@ -1007,7 +1103,7 @@ void GpuExecutor<T>::compute_batch_key() {
 template <typename T>
 bool GpuExecutor<T>::batchable() const {
   return batchEnabled_ && plan_->size == 1 && !peerWrites_ && exchChunks_ <= 1 && !capturing_ &&
-         !poison_ && interPlanes_ >= plan_->local_planes();
+         !poison_ && interPlanes_ >= plan_->local_planes() && !longX_ && !longY_ && !longZ_;
 }
 
 // A member needs no stream join when it runs on the leader's stream, or when

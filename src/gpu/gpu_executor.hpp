@@ -12,6 +12,7 @@
 
 #include "api/grid_impl.hpp"
 #include "gpu/gpu_runtime.hpp"
+#include "kernels/long_fft.hpp"
 #include "kernels/stage_args.hpp"
 #include "plan/index_plan.hpp"
 
@@ -104,6 +105,16 @@ private:
   bool floatExchange_ = false;
   long long interStride_ = 0;  // row stride of [z][column][y]
   int interPlanes_ = 1;        // planes per y/x launch pair (fits the grid's intermediate)
+  // axes beyond one workgroup's LDS: glue + global four-step / Bluestein FFT
+  bool longX_ = false, longY_ = false, longZ_ = false;
+  dev::LongPlan lpX_, lpY_, lpZ_;
+  std::unique_ptr<DeviceBuffer> longWork_[4];
+  void setup_long_axes();
+  dev::LongBufs<T> long_bufs() const;
+  void y_backward_launch(const dev::YArgs& ya, const void* slab, cx<T>* inter);
+  void y_forward_launch(const dev::YArgs& ya, cx<T>* inter, void* slab);
+  void x_backward_launch(const dev::XArgs& xa, const cx<T>* inter, void* space);
+  void x_forward_launch(const dev::XArgs& xa, const void* space, cx<T>* inter);
   cx<T>* inter_for(cx<T>* inter, int z0) const;
   bool poison_ = false;        // SPFFT_POISON=1: NaN-fill work buffers before each direction
   int deviceId_ = 0;

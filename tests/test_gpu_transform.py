@@ -984,3 +984,40 @@ def test_capped_intermediate_distributed(gpu, exchange, chunks, monkeypatch):
 
     for e in run_ranks(P, body):
         assert e < 1e-11
+
+
+# ------------------------------------------------------------- long lines
+# Axes beyond one workgroup's LDS run the global four-step engine (6144 = 64 x 96,
+# 8192 = 64 x 128, 12288) or Bluestein over it (the prime 4099: m = 16384 = 128 x 128),
+# fp64 and fp32, on the z, y and x axes, C2C and R2C (packed-real long x for even
+# lengths, hermitian-extended complex rows for odd ones).
+@pytest.mark.parametrize("dims,ttype,single", [
+    ((6, 5, 6144), "c2c", False), ((4, 6, 8192), "c2c", False), ((5, 4, 4099), "c2c", False),
+    ((6144, 4, 6), "c2c", False), ((8192, 3, 5), "c2c", False), ((4099, 4, 5), "c2c", False),
+    ((4, 6144, 5), "c2c", False), ((5, 4099, 4), "c2c", False),
+    ((4, 5, 12288), "c2c", True), ((5, 4, 4099), "c2c", True), ((12288, 3, 4), "c2c", True),
+    ((4099, 3, 4), "c2c", True), ((3, 4099, 4), "c2c", True),
+    ((12288, 4, 5), "r2c", False), ((4099, 4, 5), "r2c", False), ((6, 5, 6144), "r2c", False),
+    ((4, 4099, 5), "r2c", False), ((24576, 3, 4), "r2c", True), ((4099, 3, 4), "r2c", True),
+])
+def test_long_lines_any_length(gpu, dims, ttype, single):
+    import torch
+    rng = np.random.default_rng(4099)
+    nx, ny, nz = dims
+    r2c = ttype == "r2c"
+    idx = create_value_indices(rng, [1.0], 0.8, 0.7, nx, ny, nz, r2c)[0]
+    G = sp.GridFloat if single else sp.Grid
+    grid = G(nx, ny, nz, nx * ny, GPU, 1)
+    t = grid.create_transform(GPU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
+                              nx, ny, nz, nz, idx)
+    tol = 2e-5 if single else 1e-12
+    cdt = torch.complex64 if single else torch.complex128
+    rdt = torch.float32 if single else torch.float64
+    space = rng.standard_normal((nz, ny, nx))
+    if not r2c:
+        space = space + 1j * rng.standard_normal((nz, ny, nx))
+    f = t.forward(torch.as_tensor(space, device=gpu, dtype=rdt if r2c else cdt))
+    assert max_rel_error(f.cpu().numpy(), dense_forward(space, idx, dims, r2c=r2c)) < tol
+    vals = f.cpu().numpy().astype(np.complex128)
+    b = t.backward(f)
+    assert max_rel_error(b.cpu().numpy(), dense_backward(idx, vals, dims, r2c=r2c)) < tol
