@@ -31,8 +31,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # transforms/s of the reference's vendor-FFT calls alone on one MI355X, 256^3
-# C2C fp64 r = N/2 (tools/ref_pipeline_bench.py)
-REF_FFT_ONLY_256 = 2210.2
+# C2C fp64 r = N/2 (tools/ref_pipeline_bench.py), by the
+# number of transforms per step (T on T streams)
+REF_FFT_ONLY_256_BY_T = {1: 2210.2}
 
 
 def parse():
@@ -215,7 +216,12 @@ def main():
     # on one MI355X, an upper bound on its throughput for the headline config;
     # no measured reference exists for other configs or for N > 1 GPUs
     headline = (n == 256 and a.cutoff == 0.5 and a.type == "c2c" and not single)
-    vs_baseline = rate / REF_FFT_ONLY_256 if (headline and world == 1) else None
+    # comparator per protocol: the reference algorithm's rocFFT calls alone on one
+    # MI355X, one transform at a time (T = 1) or T transforms on T streams
+    # (tools/ref_pipeline_bench.py --transforms T), so the ratio does not mix the
+    # multi-transform overlap into the per-transform speed-up
+    ref_rate = REF_FFT_ONLY_256_BY_T.get(T) if (headline and world == 1) else None
+    vs_baseline = rate / ref_rate if ref_rate else None
     if a.timing:
         for tr in ts:  # completes the GPU stage intervals (gpu/<direction>/<stage>)
             tr.synchronize()
@@ -233,6 +239,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": vs_baseline,
+            "vs_baseline_basis": (f"value / {ref_rate:.1f}: the reference algorithm's rocFFT calls "
+                                  f"alone on one MI355X with the same {T} transform(s) per step "
+                                  f"(BASELINE.md B7, tools/ref_pipeline_bench.py --transforms {T})"
+                                  if vs_baseline else None),
             "dtype": "fp32" if single else "fp64",
             "data": "synthetic (random complex values on the spherical-cutoff index set)",
             "config": {

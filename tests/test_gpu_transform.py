@@ -871,7 +871,7 @@ def test_rccl_channel_shared_across_grids(gpu, monkeypatch):
         ts = []
         for _ in range(3):
             g = sp.Grid(nx, ny, nz, max_sticks, GPU, 1, max_local_z_length=max(planes), comm=comm,
-                        exchange_type=getattr(sp.ExchangeType, exchange))
+                        exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
             ts.append(g.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, planes[rank],
                                          parts[rank]))
         ins = [torch.as_tensor(v[starts[rank]:starts[rank + 1]], device="cuda") for v in vals]

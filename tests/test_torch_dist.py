@@ -74,6 +74,17 @@ def test_rccl_init_failure_falls_back_to_peer_writes(gpu, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_rccl_init_failure_one_rank(gpu, monkeypatch):
+    """Fault injection on one rank only (SPFFT_FAULT_RCCL_INIT=2: the last rank never
+    calls ncclCommInitRankConfig). The other rank's non-blocking initialisation waits
+    until SPFFT_COMM_TIMEOUT, aborts, and both ranks agree on the peer-write fallback
+    instead of one of them blocking inside RCCL."""
+    monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "2")
+    monkeypatch.setenv("SPFFT_COMM_TIMEOUT", "5")
+    _launch(2, "COMPACT_BUFFERED", "--iters=2", expect="ipc", timeout=180)
+
+
+@pytest.mark.gpu
 def test_rccl_init_failure_strict(gpu, monkeypatch):
     """With SPFFT_GPU_EXCHANGE=rccl there is no fallback: every rank raises MPIError
     (with the cause) instead of hanging."""

@@ -21,7 +21,11 @@ Rows printed (one JSON line each, transforms/s = 2 * steps / elapsed):
     even if its pack/unpack kernels cost nothing;
   * "dense_fftn": a dense 3D Z2Z ifftn + fftn of the full N^3 grid.
 
-Usage: python tools/ref_pipeline_bench.py [--size 256] [--cutoff 0.5] [--steps 20]
+With --transforms T, T independent copies of each row run per step, one HIP
+stream each (the comparator of bench.py's multi_transform headline, where T
+transforms per step overlap on T streams); transforms/s = 2 * T * steps / elapsed.
+
+Usage: python tools/ref_pipeline_bench.py [--size 256] [--cutoff 0.5] [--steps 20] [--transforms T]
 """
 from __future__ import annotations
 
@@ -42,6 +46,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="double", choices=["double", "single"])
+    ap.add_argument("--transforms", type=int, default=1)
     a = ap.parse_args()
 
     import numpy as np
@@ -113,19 +118,37 @@ def main():
         sync()
         err = max_rel_error((out / (X * Y * Z)).cpu().numpy(), vals.cpu().numpy())
 
+    T = max(1, a.transforms)
+    streams = [torch.cuda.Stream() for _ in range(T)] if (T > 1 and dev.type == "cuda") else []
+
+    def run(fn):
+        if not streams:
+            fn()
+            return
+        cur = torch.cuda.current_stream()
+        for st in streams:
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                fn()
+        for st in streams:
+            cur.wait_stream(st)
+
     for name, fn in (("ref_pipeline", pipeline), ("ref_fft_only", fft_only),
                      ("dense_fftn", dense_fftn)):
+        if T > 1 and name == "ref_pipeline":
+            continue  # shares its buffers across calls: one stream only
         for _ in range(a.warmup):
-            fn()
+            run(fn)
         sync()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            fn()
+            run(fn)
         sync()
         el = time.perf_counter() - t0
         rec = {"row": name, "size": n, "cutoff": a.cutoff, "precision": a.precision,
-               "transforms_per_s": 2.0 * a.steps / el, "ms_per_step": 1e3 * el / a.steps,
-               "sticks": S, "values": len(idx)}
+               "transforms_per_step": T if streams else 1,
+               "transforms_per_s": 2.0 * (T if streams else 1) * a.steps / el,
+               "ms_per_step": 1e3 * el / a.steps, "sticks": S, "values": len(idx)}
         if name == "ref_pipeline":
             rec["check_error"] = err
         print(json.dumps(rec), flush=True)
