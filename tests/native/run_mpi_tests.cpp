@@ -1,9 +1,12 @@
 // MPI tests (run with mpiexec -n P): distributed transforms over MPI_COMM_WORLD
 // for every exchange type and several stick/plane distributions against a dense
 // DFT (reference: tests/mpi_tests/test_transform.cpp, test_multi_transform.cpp).
+#include <hip/hip_runtime_api.h>
 #include <mpi.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <stdexcept>
 #include <numeric>
 
 #include "spfft/spfft.h"
@@ -146,12 +149,21 @@ SPFFT_TEST(mpi_r2c_planes_on_one_rank) {
   for (auto ex : kExchanges) run_case(ex, SPFFT_TRANS_R2C, uniform(), only(0), 11, 12, 10, true, SPFFT_PU_HOST);
 }
 SPFFT_TEST(mpi_gpu_c2c) {
-  // one GPU per rank only (RCCL data plane); skipped otherwise
+  // rank r on device r % devices: one GPU per rank uses RCCL; ranks sharing a
+  // device (the one-GPU test box) use the IPC peer-write plane
   int nd = spfft_amd_device_count();
-  int ok = nd >= g_size ? 1 : 0, all = 0;
+  int ok = nd >= 1 ? 1 : 0, all = 0;
   MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
-  if (!all) return;
-  run_case(SPFFT_EXCH_DEFAULT, SPFFT_TRANS_C2C, uniform(), uniform(), 16, 12, 32, true, SPFFT_PU_GPU);
+  if (!all) {
+    if (g_rank == 0) std::printf("SKIP mpi_gpu_c2c: no GPU on some rank\n");
+    return;
+  }
+  if (hipSetDevice(g_rank % nd) != hipSuccess) throw std::runtime_error("hipSetDevice");
+  for (auto ex : kExchanges) {
+    run_case(ex, SPFFT_TRANS_C2C, uniform(), uniform(), 16, 12, 32, true, SPFFT_PU_GPU);
+    run_case(ex, SPFFT_TRANS_C2C, only(0), only(g_size - 1), 12, 13, 11, false, SPFFT_PU_GPU);
+  }
+  run_case(SPFFT_EXCH_DEFAULT, SPFFT_TRANS_R2C, uniform(), uniform(), 12, 11, 13, false, SPFFT_PU_GPU);
 }
 SPFFT_TEST(mpi_parameter_mismatch) {
   // ranks disagree on the exchange type -> every rank gets MPIParameterMismatchError
