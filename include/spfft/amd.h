@@ -63,6 +63,10 @@ SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchan
  * grid). Collective on first call (creates the data plane). */
 SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name);
+/* Device memory a grid allocated (exchange buffers, intermediate, space domain). */
+SPFFT_EXPORT SpfftError spfft_amd_grid_device_bytes(SpfftGrid grid, unsigned long long* bytes);
+SPFFT_EXPORT SpfftError spfft_amd_float_grid_device_bytes(SpfftFloatGrid grid,
+                                                          unsigned long long* bytes);
 /* Number of RCCL communicators this process has created. Grids whose
  * communicators have the same members on the same devices share one
  * (SPFFT_RCCL_SHARE=0: one per grid). */

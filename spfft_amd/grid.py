@@ -156,6 +156,13 @@ class _GridBase:
         return v.value.decode()
 
     @property
+    def device_bytes(self) -> int:
+        """Device memory the grid allocated (exchange buffers, y/x intermediate, space)."""
+        v = ctypes.c_ulonglong()
+        _check(self._prec.amd_fn("grid_device_bytes")(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
     def communicator(self):
         return self._comm
 

@@ -364,6 +364,15 @@ SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** nam
   return with_handle<GridFloat>(grid, [&](GridFloat& g) { *name = data_plane_of(*g.impl()); });
 }
 
+SpfftError spfft_amd_grid_device_bytes(SpfftGrid grid, unsigned long long* bytes) {
+  if (!bytes) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<Grid>(grid, [&](Grid& g) { *bytes = g.impl()->device_bytes(); });
+}
+SpfftError spfft_amd_float_grid_device_bytes(SpfftFloatGrid grid, unsigned long long* bytes) {
+  if (!bytes) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<GridFloat>(grid, [&](GridFloat& g) { *bytes = g.impl()->device_bytes(); });
+}
+
 SpfftError spfft_amd_rccl_communicators(int* count) {
   if (!count) return SPFFT_INVALID_PARAMETER_ERROR;
   *count = spfft::DeviceComm::rccl_channels_created();

@@ -38,7 +38,12 @@ void GridImpl<T>::init(int maxDimX, int maxDimY, int maxDimZ, int maxSticks, int
   // 64-bit sizes; the public API keeps int (reference quirk: int views, gpu_array_view.hpp:71)
   // room for row / stick padding (kMaxPad elements per row or stick)
   planeElems_ = checked_mul(checked_mul(maxX_, maxY_ + kMaxPad), std::max(1, maxLocalZ_));
-  exchElems_ = std::max(planeElems_, checked_mul(maxZ_ + kMaxPad, maxSticks_));
+  // exchange sides sized for what they hold, not for a slab (the reference
+  // sizes both arrays max(Nx Ny Lmax, Nz Smax), grid_internal.cpp:198-202):
+  // stick side = local sticks x (dimZ + pad); slab side (distributed) = all
+  // ranks' sticks x local planes (set by the distributed constructor)
+  exchElems_ = std::max<i64>(1, checked_mul(maxZ_ + kMaxPad, maxSticks_));
+  slabElems_ = exchElems_;
   {
     const char* e = std::getenv("SPFFT_INTER_BYTES");
     const double capBytes = e && *e ? std::atof(e) : 2.0 * (1 << 30);
@@ -84,6 +89,7 @@ GridImpl<T>::GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZCol
   std::vector<Info> all(comm_->size());
   comm_->allgather(&mine, all.data(), sizeof(Info));
   int gMaxSticks = 0, gMaxLocalZ = 0;
+  i64 sumSticks = 0;
   for (const auto& i : all) {
     if (i.status) {
       if (status) throw InvalidParameterError();
@@ -92,12 +98,17 @@ GridImpl<T>::GridImpl(int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZCol
     if (i.pu != mine.pu || i.exch != mine.exch) throw MPIParameterMismatchError();
     gMaxSticks = std::max(gMaxSticks, i.maxSticks);
     gMaxLocalZ = std::max(gMaxLocalZ, i.maxLocalZ);
+    sumSticks += i.maxSticks;
   }
   exchange_ = exchangeType == SPFFT_EXCH_DEFAULT ? SPFFT_EXCH_COMPACT_BUFFERED : exchangeType;
   init(maxDimX, maxDimY, maxDimZ, maxNumLocalZColumns, maxLocalZLength, pu, numThreads);
-  if (comm_->size() > 1 && is_exchange_buffered(exchange_)) {
-    const i64 padded = checked_mul(checked_mul(gMaxSticks, gMaxLocalZ), comm_->size());
-    exchElems_ = std::max(exchElems_, padded);
+  if (comm_->size() > 1) {
+    slabElems_ = std::max<i64>(1, checked_mul(sumSticks, std::max(1, maxLocalZ_)));
+    if (is_exchange_buffered(exchange_)) {
+      const i64 padded = checked_mul(checked_mul(gMaxSticks, gMaxLocalZ), comm_->size());
+      exchElems_ = std::max(exchElems_, padded);
+      slabElems_ = std::max(slabElems_, padded);
+    }
   }
   if (pu_ & SPFFT_PU_GPU) allocate_device();
 }
@@ -115,6 +126,7 @@ GridImpl<T>::GridImpl(const GridImpl& o)
       exchange_(o.exchange_),
       comm_(o.comm_ ? o.comm_->duplicate() : nullptr),
       exchElems_(o.exchElems_),
+      slabElems_(o.slabElems_),
       planeElems_(o.planeElems_),
       interDevElems_(o.interDevElems_) {
   if (pu_ & SPFFT_PU_GPU) {
@@ -147,9 +159,17 @@ template <typename T>
 void GridImpl<T>::allocate_device() {
   const std::size_t cb = sizeof(T) * 2;
   dev_[kStickSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
-  if (!local()) dev_[kSlabSide].reset(new DeviceBuffer(static_cast<std::size_t>(exchElems_) * cb));
+  if (!local()) dev_[kSlabSide].reset(new DeviceBuffer(static_cast<std::size_t>(slabElems_) * cb));
   dev_[kInter].reset(new DeviceBuffer(static_cast<std::size_t>(interDevElems_) * cb));
   dev_[kSpace].reset(new DeviceBuffer(static_cast<std::size_t>(planeElems_) * cb));
+}
+
+template <typename T>
+std::size_t GridImpl<T>::device_bytes() const {
+  std::size_t b = 0;
+  for (const auto& d : dev_)
+    if (d) b += d->bytes();
+  return b;
 }
 
 template <typename T>

@@ -50,18 +50,26 @@ public:
 
   // Buffer slots (complex<T> element counts fixed at construction).
   enum Slot { kStickSide = 0, kSlabSide = 1, kInter = 2, kSpace = 3, kNumSlots = 4 };
-  i64 slot_elements(Slot s) const { return s == kStickSide || s == kSlabSide ? exchElems_ : planeElems_; }
+  i64 slot_elements(Slot s) const {
+    if (s == kStickSide) return exchElems_;
+    if (s == kSlabSide) return local() ? exchElems_ : slabElems_;
+    return planeElems_;
+  }
   // Device allocation of a slot. The [z][column][y] intermediate of the GPU
   // y/x stages is capped (SPFFT_INTER_BYTES, default 2 GiB, at least one
   // plane): larger slabs run the y/x stages in plane ranges that reuse it, so
-  // a GPU grid holds ~3 slab-sized buffers when distributed and ~2 when local
-  // instead of 4 / 3 (reference: 2 arrays, src/spfft/grid_internal.cpp:185-221).
+  // a GPU grid holds the exchange sides (sized by sticks, tools/memory_model.py),
+  // the space domain and a bounded intermediate (reference: 2 slab-sized
+  // arrays, src/spfft/grid_internal.cpp:185-221).
   i64 device_slot_elements(Slot s) const { return s == kInter ? interDevElems_ : slot_elements(s); }
 
   // Host memory (allocated on first use; pinned if the grid has the GPU bit).
   void* host_slot(Slot s);
   // Device memory (GPU grids only).
   void* device_slot(Slot s);
+
+  // Bytes of device memory the grid allocated (exchange sides, intermediate, space).
+  std::size_t device_bytes() const;
 
   // RCCL / peer-copy data plane (GPU distributed grids), created on first use.
   DeviceComm& device_comm();
@@ -80,7 +88,7 @@ private:
   int deviceId_ = 0;
   SpfftExchangeType exchange_ = SPFFT_EXCH_COMPACT_BUFFERED;
   std::shared_ptr<Communicator> comm_;
-  i64 exchElems_ = 0, planeElems_ = 0, interDevElems_ = 0;
+  i64 exchElems_ = 0, slabElems_ = 0, planeElems_ = 0, interDevElems_ = 0;
 
   std::unique_ptr<ThreadPool> pool_;
   HostBuffer host_[kNumSlots];

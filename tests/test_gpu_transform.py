@@ -1021,3 +1021,29 @@ def test_long_lines_any_length(gpu, dims, ttype, single):
     vals = f.cpu().numpy().astype(np.complex128)
     b = t.backward(f)
     assert max_rel_error(b.cpu().numpy(), dense_backward(idx, vals, dims, r2c=r2c)) < tol
+
+
+def test_grid_device_footprint(gpu):
+    """Grid memory (tools/memory_model.py): stick side (dimZ + 32) x maxSticks, slab
+    side sum(maxSticks) x maxLocalZ (distributed only), space maxX (maxY + 32) maxLocalZ,
+    intermediate min(that, 2 GiB); complex elements. A local 64^3 grid with a sphere's
+    sticks holds ~1.8 slabs, 4 virtual ranks ~2.6 slabs each."""
+    import torch
+    from spfft_amd.parallel import run_ranks
+    n = 64
+    sticks = 3217
+    g = sp.Grid(n, n, n, sticks, GPU, 1)
+    plane = n * (n + 32) * n
+    assert g.device_bytes == 16 * ((n + 32) * sticks + 2 * plane)
+    P = 4
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        gd = sp.Grid(n, n, n, sticks // P + 1, GPU, 1, max_local_z_length=n // P, comm=comm,
+                     exchange_type=sp.ExchangeType.COMPACT_BUFFERED)
+        pl = n * (n + 32) * (n // P)
+        want = 16 * ((n + 32) * (sticks // P + 1) + P * (sticks // P + 1) * (n // P) + 2 * pl)
+        return gd.device_bytes, want
+
+    for got, want in run_ranks(P, body):
+        assert got == want

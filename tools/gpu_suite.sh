@@ -45,6 +45,7 @@ prof() {  # prof <name> <bench args...>
 }
 
 PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread"
+ncmd=0
 for s in "$@"; do
   case "$s" in
     tests) step gpu_tests 1000 $PYT tests -m gpu -q ;;
@@ -68,7 +69,7 @@ for s in "$@"; do
       SPFFT_GPU_EXCHANGE=rccl NCCL_DEBUG=WARN step rccl_shared_device 180 \
         python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
         --master-port=29561 tools/rccl_probe.py COMPACT_BUFFERED --iters=2 ;;
-    cmd:*) step cmd 900 bash -c "${s#cmd:}" ;;
+    cmd:*) ncmd=$((ncmd + 1)); step cmd$ncmd 900 bash -c "${s#cmd:}" ;;
     *) echo "unknown suite $s"; exit 2 ;;
   esac
 done
