@@ -33,7 +33,7 @@ sys.path.insert(0, REPO)
 # transforms/s of the reference's vendor-FFT calls alone on one MI355X, 256^3
 # C2C fp64 r = N/2 (tools/ref_pipeline_bench.py), by the
 # number of transforms per step (T on T streams)
-REF_FFT_ONLY_256_BY_T = {1: 2210.2}
+REF_FFT_ONLY_256_BY_T = {1: 2210.2, 4: 2418.3}  # profiles/r3/comparator/
 
 
 def parse():

@@ -168,7 +168,7 @@ void GpuExecutor<T>::log_plan() const {
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
                "y{%s} x{%s}%s inter_planes=%d | exchange=%s%s plane=%s chunks=%d (%.2f MB per "
-               "peer) peer_writes=%d\n",
+               "peer) peer_writes=%d peer_offsets=[%lld, %lld]\n",
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
@@ -176,7 +176,7 @@ void GpuExecutor<T>::log_plan() const {
                describe(longX_, lpX_, twXh_ ? p.dimX / 2 : p.dimX, true).c_str(),
                twXh_ ? " packed-real" : "", interPlanes_, layout_.buffered ? "buffered" : "compact",
                floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, chunkModel_ / 1e6,
-               peerWrites_ ? 1 : 0);
+               peerWrites_ ? 1 : 0, peerOffsetRange_[0], peerOffsetRange_[1]);
 }
 
 template <typename T>
@@ -395,6 +395,17 @@ void GpuExecutor<T>::build_peer_tables() {
     cb[k] = base[p.colRank[k]] + static_cast<i64>(p.colLocal[k]) * layout_.slabStride;
   upload(colBaseRemote_, cb);
   build_col_desc(colDescRemote_, cb, layout_.slabStride);
+  // peers' buffers are addressed as element offsets from the local ones: both
+  // signs occur (the descriptor and list paths take signed 64-bit bases)
+  peerOffsetRange_[0] = peerOffsetRange_[1] = 0;
+  for (long long v : seg) {
+    peerOffsetRange_[0] = std::min(peerOffsetRange_[0], v);
+    peerOffsetRange_[1] = std::max(peerOffsetRange_[1], v);
+  }
+  for (long long v : base) {
+    peerOffsetRange_[0] = std::min(peerOffsetRange_[0], v);
+    peerOffsetRange_[1] = std::max(peerOffsetRange_[1], v);
+  }
 }
 
 template <typename T>

@@ -168,6 +168,7 @@ private:
   bool localDirect_ = false;
   long long slab_offset() const;
   std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
+  long long peerOffsetRange_[2] = {0, 0};  // min / max remote base (SPFFT_LOG)
 
   // Pipelined exchange (RCCL / loopback data planes, compact layout): every
   // rank's planes are split into K chunks and both exchange buffers are laid

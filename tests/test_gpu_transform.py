@@ -1047,3 +1047,40 @@ def test_grid_device_footprint(gpu):
 
     for got, want in run_ranks(P, body):
         assert got == want
+
+
+def test_peer_write_offsets_both_signs(gpu, monkeypatch, capfd):
+    """Peer-write plans address the peers' buffers as signed element offsets from the
+    local ones (round 2's y base table dropped negative ones). Three virtual ranks
+    allocate in rank order, so rank 0 sees positive and rank 2 negative offsets; the
+    transform must be exact with both (SPFFT_LOG prints each plan's offset range)."""
+    import re
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    monkeypatch.setenv("SPFFT_LOG", "1")
+    dims = (20, 18, 16)
+    gidx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(2)
+    vals = _rand_vals(rng, len(gidx))
+    ref = dense_backward(gidx, vals, dims)
+    parts = distribute_sticks(gidx, 3, dims)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU,
+                             exchange_type=sp.ExchangeType.UNBUFFERED)
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.as_tensor(vals[start:start + len(s.indices)], device="cuda")
+        e1 = max_rel_error(s.transform.backward(v).cpu().numpy(),
+                           ref[s.z_offset:s.z_offset + s.z_length])
+        e2 = max_rel_error(s.transform.forward(None, scaling=sp.Scaling.FULL).cpu().numpy(),
+                           v.cpu().numpy())
+        return max(e1, e2)
+
+    for e in run_ranks(3, body):
+        assert e < 1e-12
+    err = capfd.readouterr().err
+    ranges = [(int(a), int(b)) for a, b in re.findall(r"peer_offsets=\[(-?\d+), (-?\d+)\]", err)]
+    assert len(ranges) == 3, err[-2000:]
+    assert min(r[0] for r in ranges) < 0 < max(r[1] for r in ranges), ranges
