@@ -301,6 +301,10 @@ __host__ __device__ constexpr int lf_lines(int b) {
 #ifndef SPFFT_LF_STRIDE
 #define SPFFT_LF_STRIDE 1
 #endif
+// FftCT: fetch a pass's twiddles before the LDS exchange that precedes it
+#ifndef SPFFT_TW_PREFETCH
+#define SPFFT_TW_PREFETCH 1
+#endif
 // Line stride of the line-fast mapping: a 16-lane LDS access group (64 banks x
 // 4 B = 16 slots of 16 B for fp64, 32 slots of 8 B for fp32) holds lines
 // b = 0..B-1 at kMod/B consecutive lane positions t; with the stride
@@ -317,7 +321,7 @@ __host__ __device__ constexpr int lf_padded_stride(int n, int b) {
 //  false: t fastest (a line's TP lanes adjacent; row-contiguous global access),
 //  true:  b fastest (B lines adjacent; column-contiguous global access, e.g. a
 //         stick's z-run or an intermediate column's y-run).
-template <typename T, int N, int S, bool LF = false>
+template <typename T, int N, int S, bool LF = false, bool TwPre = true>
 struct FftCT {
   // line-fast engines (column access) take the precision-specific shape; the
   // row-mapped engine of the z stage keeps the default (fewer VGPRs per lane);
@@ -386,6 +390,34 @@ struct FftCT {
     }
   }
 
+  // Twiddles of a pass, fetched into registers ahead of the pass: their loads
+  // are issued before the LDS exchange that precedes the pass, so the table
+  // read (an L1/L2 hit) overlaps the exchange instead of following it.
+  // (not for the 32-element shapes of N = 1024: their registers are full)
+  static constexpr bool kTwPrefetch = SPFFT_TW_PREFETCH && TwPre && E <= 16;
+  template <int R, int NS>
+  struct PassTw {
+    cx<TwT> w[(E / R) * (R - 1)];
+  };
+  template <int R, int NS>
+  __device__ static void fetch_tw(PassTw<R, NS>& p, int t, const cx<TwT>* __restrict__ tw) {
+#pragma unroll
+    for (int k = 0; k < E / R; ++k) {
+      const int kk = (t + k * TP) % NS;
+#pragma unroll
+      for (int r = 1; r < R; ++r) p.w[k * (R - 1) + r - 1] = tw[kk * r * (N / (NS * R))];
+    }
+  }
+  template <int R, int NS>
+  __device__ static void compute_tw(cx<T> (&v)[E], const PassTw<R, NS>& p) {
+#pragma unroll
+    for (int k = 0; k < E / R; ++k) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], p.w[k * (R - 1) + r - 1]);
+      Dft<R, S, T>::run(&v[k * R]);
+    }
+  }
+
   template <class Load>
   __device__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<TwT>* __restrict__ tw,
                                    Load load, int b, int t) {
@@ -402,13 +434,28 @@ struct FftCT {
       }
     }
     compute<Sh::R0, 1>(v, t, tw);
-    if constexpr (Sh::R1 > 1) {
-      exchange<Sh::R0, 1, Sh::R1>(v, line, t);
-      compute<Sh::R1, Sh::R0>(v, t, tw);
-    }
-    if constexpr (Sh::R2 > 1) {
-      exchange<Sh::R1, Sh::R0, Sh::R2>(v, line, t);
-      compute<Sh::R2, Sh::R0 * Sh::R1>(v, t, tw);
+    if constexpr (kTwPrefetch) {
+      if constexpr (Sh::R1 > 1) {
+        PassTw<Sh::R1, Sh::R0> p1;
+        fetch_tw(p1, t, tw);
+        exchange<Sh::R0, 1, Sh::R1>(v, line, t);
+        compute_tw(v, p1);
+      }
+      if constexpr (Sh::R2 > 1) {
+        PassTw<Sh::R2, Sh::R0 * Sh::R1> p2;
+        fetch_tw(p2, t, tw);
+        exchange<Sh::R1, Sh::R0, Sh::R2>(v, line, t);
+        compute_tw(v, p2);
+      }
+    } else {
+      if constexpr (Sh::R1 > 1) {
+        exchange<Sh::R0, 1, Sh::R1>(v, line, t);
+        compute<Sh::R1, Sh::R0>(v, t, tw);
+      }
+      if constexpr (Sh::R2 > 1) {
+        exchange<Sh::R1, Sh::R0, Sh::R2>(v, line, t);
+        compute<Sh::R2, Sh::R0 * Sh::R1>(v, t, tw);
+      }
     }
   }
 
@@ -419,6 +466,19 @@ struct FftCT {
   // on it (asserted there in debug builds).
   __device__ static int lane_line() { return LF ? threadIdx.x % B : threadIdx.x / TP; }
   __device__ static int lane_pos() { return LF ? threadIdx.x / B : threadIdx.x % TP; }
+
+  // The positions run() hands to store(), in call order: call i of store()
+  // receives position pos of fn(i, pos) (kStoreSlots calls, all unrolled).
+  static constexpr int kStoreSlots = E;
+  template <class Fn>
+  __device__ static void for_each_store_pos(Fn fn) {
+    const int t = lane_pos();
+#pragma unroll
+    for (int k = 0; k < E / RL; ++k) {
+#pragma unroll
+      for (int r = 0; r < RL; ++r) fn(k * RL + r, t + k * TP + r * (N / RL));
+    }
+  }
 
   template <class Load, class Store>
   __device__ static void run(cx<T>* lds, const cx<TwT>* __restrict__ tw, Load load, Store store) {
@@ -673,9 +733,9 @@ struct FftMR {
 };
 
 // Compile-time engine core of a length: FftCT for powers of two, else FftMR.
-template <typename T, int N, int S, bool LF>
+template <typename T, int N, int S, bool LF, bool TwPre = true>
 struct CtCore {
-  using type = typename std::conditional<(N & (N - 1)) == 0, FftCT<T, N, S, LF>,
+  using type = typename std::conditional<(N & (N - 1)) == 0, FftCT<T, N, S, LF, TwPre>,
                                          FftMR<T, N, S, LF>>::type;
 };
 

@@ -166,9 +166,13 @@ __device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, S
 }
 
 // ------------------------------------------------------------ engine adapters
-template <typename T, int N, int S, bool LF = false>
+// TwPre: the FftCT twiddle prefetch (off for the kernels where its registers
+// cost occupancy: the fp32 y forward kernels measured 61 -> 65 us at 256^3 and
+// 260 -> 384 us at 512^3 with it, 129+ VGPRs, one 512-thread workgroup per CU)
+template <typename T, int N, int S, bool LF = false, bool TwPre = true>
 struct CtEng {
-  using F = typename CtCore<T, N, S, LF>::type;
+  using F = typename CtCore<T, N, S, LF, TwPre>::type;
+  static constexpr int kN = N;
   static constexpr bool kBatchedCopy = false;
   static constexpr bool kLineFast = LF;
   static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
@@ -418,6 +422,14 @@ __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
   return a.segDispl[r] + static_cast<long long>(s) * a.segStride[r] + (pos - a.segZOff[r]);
 }
 
+// A workgroup-uniform value materialised in a scalar register at this point:
+// the compiler may not sink its (scalar) load into later branches.
+__device__ __forceinline__ int pin_uniform(int v) {
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
 #define SPFFT_LDS_DECL(T)                                         \
   extern __shared__ __attribute__((aligned(16))) char spfftSmem[]; \
   cx<T>* lds = reinterpret_cast<cx<T>*>(spfftSmem)
@@ -650,6 +662,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
 }
 
+#ifndef SPFFT_ZB_REGDESC
+#define SPFFT_ZB_REGDESC 1
+#endif
+
 // z stage for "simple" sticks (values of a stick contiguous, <= 2 z-runs; the
 // common stick-major input): every lane maps its FFT positions z straight to
 // value offsets, so values are loaded into registers and written back with
@@ -701,7 +717,28 @@ __global__ void __launch_bounds__(Eng::kBlock)
     hermitian_lines(eng, lds, a.zeroStick - s0, 1, n);
     eng.lds_to_global(lds, tw, store);
   } else {
+#if SPFFT_ZB_REGDESC
+    // compile-time engines load only the lane's own line (b == lane_line(),
+    // the FftCT/FftMR contract): its descriptor is read from LDS once into
+    // registers and the value offset is a branch-free select. Reading d[b] in
+    // the load lambda re-read the descriptor from LDS for every element, each
+    // read waited out before the dependent value load could issue.
+    const int lb = Eng::F::lane_line();
+    StickDesc q = d[lb < nl ? lb : 0];
+    int z0 = q.z0, len0 = q.len0, z1 = q.z1, len1 = q.count - q.len0, vs = q.valueStart;
+    if (lb >= nl) len0 = len1 = 0;
+    asm volatile("" : "+v"(z0), "+v"(len0), "+v"(z1), "+v"(len1), "+v"(vs));
+    const cx<T>* vals = values + vs;
+    eng.global_to_global(lds, tw, [&](int, int z) -> cx<T> {
+      const unsigned j0 = static_cast<unsigned>(z - z0), j1 = static_cast<unsigned>(z - z1);
+      const bool in0 = j0 < static_cast<unsigned>(len0);
+      const bool in1 = j1 < static_cast<unsigned>(len1);
+      const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
+      return (in0 || in1) ? ld_values(&vals[j]) : czero<T>();
+    }, store);
+#else
     eng.global_to_global(lds, tw, load, store);
+#endif
   }
   release_remote(a.remote);
 }
@@ -796,29 +833,62 @@ __device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride
 // Every kernel keeps a single FFT call site whichever source is used: the
 // run-time engines inline their whole pass switch per call site, and a second
 // copy doubled their register demand (profiles/r2_s1/rt_regression.txt).
+#ifndef SPFFT_Y_TABLE
+#define SPFFT_Y_TABLE 1
+#endif
+#ifndef SPFFT_YF_TABLE
+#define SPFFT_YF_TABLE 1
+#endif
+// engines whose store positions can be enumerated ahead of run() (FftCT)
+template <class Eng, class = void>
+struct has_store_pos : std::false_type {};
+template <class Eng>
+struct has_store_pos<Eng, std::void_t<decltype(Eng::F::kStoreSlots)>> : std::true_type {};
 template <class Eng>
 struct ColEntries {
   bool useDesc;
   ColDesc d;
   long long stride;
+  long long* yBase;  // LDS: y -> stick-side base or -1 (table mode)
   long long* cBase;  // LDS: colBase per entry (list mode)
   int* yEnt;         // LDS: y -> entry or -1 (list mode)
   int* cY;           // LDS: entry -> y (list mode)
   int ne;
-  __device__ ColEntries(const Eng& eng, const YArgs& a, void* ldsBase, int c, bool allowDesc) {
+  // table: build only yBase, the y -> base table (the backward y stage's loads
+  // then cost one LDS read per element instead of a descriptor search per
+  // element and lane); it shares its LDS with the list-mode arrays, which the
+  // table mode does not use
+  __device__ ColEntries(const Eng& eng, const YArgs& a, void* ldsBase, int c, bool allowDesc,
+                        bool table = false) {
     const int n = eng.n();
     useDesc = allowDesc && a.colDesc != nullptr;
     stride = a.colStride;
-    cBase = reinterpret_cast<long long*>(reinterpret_cast<char*>(ldsBase) + eng.lds_bytes());
+    char* base = reinterpret_cast<char*>(ldsBase) + eng.lds_bytes();
+    yBase = reinterpret_cast<long long*>(base);
+    cBase = yBase;
     yEnt = reinterpret_cast<int*>(cBase + n);
     cY = yEnt + n;
     ne = 0;
     if (useDesc) {
       d = a.colDesc[c];
+      if (table) {
+        for (int y = threadIdx.x; y < n; y += blockDim.x) {
+          long long b;
+          yBase[y] = col_desc_find(d, stride, y, b) ? b : -1;
+        }
+        __syncthreads();
+      }
       return;
     }
     const int k0 = a.colOffsets[c];
     ne = a.colOffsets[c + 1] - k0;
+    if (table) {
+      for (int y = threadIdx.x; y < n; y += blockDim.x) yBase[y] = -1;
+      __syncthreads();
+      for (int e = threadIdx.x; e < ne; e += blockDim.x) yBase[a.colY[k0 + e]] = a.colBase[k0 + e];
+      __syncthreads();
+      return;
+    }
     for (int y = threadIdx.x; y < n; y += blockDim.x) yEnt[y] = -1;
     __syncthreads();
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {
@@ -838,15 +908,39 @@ struct ColEntries {
   }
 };
 
-// LDS the y-stage kernels reserve behind the FFT lines for ColEntries' list
-// mode (colBase, y -> entry, entry -> y). With column run descriptors only the
-// backward R2C x = 0 column (hermitian fill, list mode) needs it; C2C plans
-// skip it, which keeps fp32 N = 256 at 4 workgroups per CU instead of 3.
-inline std::size_t col_entries_lds(const YArgs& a, bool backward) {
+// LDS the y-stage kernels reserve behind the FFT lines for ColEntries: the list
+// mode (colBase, y -> entry, entry -> y) where it can run, and the y -> base
+// table (table: the kernel runs table mode; both share one region). With column
+// run descriptors only the backward R2C x = 0 column (hermitian fill) runs list
+// mode; C2C forward plans reserve nothing, which keeps fp32 N = 256 at 4
+// workgroups per CU.
+inline std::size_t col_entries_lds(const YArgs& a, bool backward, bool table = false) {
   const bool list = !a.colDesc || (backward && a.colOfX0 >= 0);
-  if (list) return std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
-  return 0;
+  std::size_t bytes = list ? std::size_t(a.n) * (sizeof(long long) + 2 * sizeof(int)) : 0;
+  if (table) bytes = std::max(bytes, std::size_t(a.n) * sizeof(long long));
+  return bytes ? bytes + 16 : 0;
 }
+
+constexpr std::size_t kLdsPerWorkgroup = 160 * 1024;
+
+// Whether a y-stage kernel with engine Eng runs table mode: compile-time
+// engines (one LDS read per element replaces their per-element search) whose
+// FFT lines leave room for the table next to the list-mode arrays.
+template <class Eng, bool Enabled>
+constexpr bool y_table() {
+  if constexpr (Eng::kBatchedCopy || !Enabled) {
+    return false;
+  } else {
+    constexpr int n = Eng::kN;
+    return Eng::F::lds_bytes() + std::size_t(n) * (sizeof(long long) + 2 * sizeof(int)) + 16 <=
+           kLdsPerWorkgroup;
+  }
+}
+
+// Source of the loads that find no stick entry (zeros): the backward y stage
+// loads every element unconditionally, from the stick side or from here, so the
+// lane's table reads and loads issue back to back with no branch per element.
+static __device__ __attribute__((aligned(64))) double gZeroSource[8] = {};
 
 // Backward y stage with the line-fast engine: lane (line = plane zz, pos = y)
 // loads straight from the stick side — consecutive lanes read consecutive z
@@ -864,11 +958,19 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   const bool x0 = c == a.colOfX0;
-  const ColEntries<Eng> ce(eng, a, lds, c, !x0);
+  constexpr bool kTable = y_table<Eng, SPFFT_Y_TABLE>();
+  const ColEntries<Eng> ce(eng, a, lds, c, !x0, kTable && !x0);
+  const BT* zsrc = reinterpret_cast<const BT*>(gZeroSource);
   auto load = [&](int b, int pos) -> cx<T> {
-    long long base;
-    if (!ce.find(pos, base) || b >= zl) return czero<T>();
-    return cvt<T>(ld_stream(&in[base + z0 + b]));
+    if constexpr (kTable) {
+      const long long base = ce.yBase[pos];
+      const BT* p = (base >= 0 && b < zl) ? in + (base + z0 + b) : zsrc;
+      return cvt<T>(ld_stream(p));
+    } else {
+      long long base;
+      if (!ce.find(pos, base) || b >= zl) return czero<T>();
+      return cvt<T>(ld_stream(&in[base + z0 + b]));
+    }
   };
   // the x = 0 column of an R2C transform: gathered into LDS, hermitian fill
   auto stage_x0 = [&]() {
@@ -923,11 +1025,28 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
-  const ColEntries<Eng> ce(eng, a, lds, c, true);
+  constexpr bool kTable = y_table<Eng, SPFFT_YF_TABLE && has_store_pos<Eng>::value>();
+  const ColEntries<Eng> ce(eng, a, lds, c, true, kTable);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
     return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_row(a, c) + pos]);
   };
+  if constexpr (kTable) {
+    // compile-time engines: the stick bases of the lane's output positions are
+    // read from the y -> base table before the FFT (their LDS latency overlaps
+    // the row loads); the stores then need no descriptor search per element
+    using F = typename Eng::F;
+    long long bases[F::kStoreSlots];
+    F::for_each_store_pos([&](int i, int pos) { bases[i] = ce.yBase[pos]; });
+    int slot = 0;
+    stage_rows(eng, lds, zl, n, load);
+    eng.lds_to_global(lds, tw, [&](int b, int, cx<T> v) {
+      const long long base = bases[slot++];
+      if (base >= 0 && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+    });
+    release_remote(a.remote);
+    return;
+  }
   auto store = [&](int b, int pos, cx<T> v) {
     long long base;
     if (ce.find(pos, base) && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
@@ -986,14 +1105,20 @@ __global__ void __launch_bounds__(Eng::kBlock)
   build_xcol(a, xCol, n);
   const cx<T>* src = inter + static_cast<long long>(zl) * a.interZStride + y0;
   const int yl = min(B, a.Y - y0);
+  // kernel arguments the per-element loads use, pinned in scalar registers up
+  // front (left to the compiler, their scalar loads were sunk into every
+  // element's branch, each waited out before that element's load could issue)
+  const int rowStride = pin_uniform(static_cast<int>(a.interStride)), nFreq = pin_uniform(a.nFreq);
+  const int dense = pin_uniform(x_dense(a) ? 1 : 0);
+  auto col_of = [&](int x) { return dense ? (x < nFreq ? x : -1) : xCol[x]; };
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= yl) return czero<T>();
-    if (R2C && pos >= a.nFreq) {
-      const int c = xcol_of(a, xCol, n - pos);
-      return c < 0 ? czero<T>() : conj(ld_inter(&src[inter_row(a, c) + b]));
+    if (R2C && pos >= nFreq) {
+      const int c = col_of(n - pos);
+      return c < 0 ? czero<T>() : conj(ld_inter(&src[c * rowStride + b]));
     }
-    const int c = xcol_of(a, xCol, pos);
-    return c < 0 ? czero<T>() : ld_inter(&src[inter_row(a, c) + b]);
+    const int c = col_of(pos);
+    return c < 0 ? czero<T>() : ld_inter(&src[c * rowStride + b]);
   };
   const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   eng.global_to_lds(lds, tw, load);
@@ -1078,9 +1203,12 @@ __global__ void __launch_bounds__(Eng::kBlock)
     // pre-pass folded into the FFT's first-pass loads: the lane that needs Z[k]
     // loads X[k] and X[h-k] itself (the mirror column is the same workgroup's
     // data, so its second read is served by the caches; plain loads keep it there)
+    // arguments of the per-element loads pinned in scalar registers (see x_backward_kernel)
+    const int rowStride = pin_uniform(static_cast<int>(a.interStride)), nFreq = pin_uniform(a.nFreq);
+    const int dense = pin_uniform(x_dense(a) ? 1 : 0);
     auto col = [&](int k, int b) -> cx<T> {
-      const int c = xcol_of(a, xCol, k);
-      return (c < 0 || b >= yl) ? czero<T>() : src[inter_row(a, c) + b];
+      const int c = dense ? (k < nFreq ? k : -1) : xCol[k];
+      return (c < 0 || b >= yl) ? czero<T>() : src[c * rowStride + b];
     };
     eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
       cx<T> xk = col(k, b);
@@ -1207,12 +1335,12 @@ inline void prepare_kernel(K kernel, std::size_t ldsBytes) {
 
 // Calls f(engine, threads, lines, ldsBytes) with the CT engine of length n if
 // there is one, else with the RT engine.
-template <typename T, int S, bool LF = false, class F>
+template <typename T, int S, bool LF = false, bool TwPre = true, class F>
 inline void with_engine(int n, F&& f) {
   switch (n) {
 #define SPFFT_CT_CASE(NN)                                                         \
   case NN: {                                                                      \
-    using E = CtEng<T, NN, S, LF>;                                                \
+    using E = CtEng<T, NN, S, LF, TwPre>;                                                \
     f(E{}, E::h_threads(), E::h_lines(), E::h_lds());                             \
     return;                                                                       \
   }

@@ -27,8 +27,10 @@ def _free_port():
 
 
 def _launch(nproc, *args, timeout=300, expect=None):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", PROBE, *args]
+    # standalone rendezvous: the launcher binds its own free port (a port picked
+    # here and released could be taken again before the launcher binds it)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={nproc}", PROBE, *args]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
     out = r.stdout + r.stderr

@@ -69,6 +69,19 @@ for s in "$@"; do
       SPFFT_GPU_EXCHANGE=rccl NCCL_DEBUG=WARN step rccl_shared_device 180 \
         python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
         --master-port=29561 tools/rccl_probe.py COMPACT_BUFFERED --iters=2 ;;
+    ab:*)
+      # ab:<v1>,<v2>,...: kernel stats of the headline fp64, 256^3 fp32 and 512^3 R2C
+      # fp32 problems (one transform per step) for the main library ("main") and the
+      # variants built by tools/build_variants.py
+      IFS=, read -r -a vs <<< "${s#ab:}"
+      for v in "${vs[@]}"; do
+        if [ "$v" = main ]; then unset SPFFT_AMD_LIBRARY; else
+          export SPFFT_AMD_LIBRARY=$PWD/spfft_amd/_native/variants/libspfft_amd_$v.so; fi
+        prof "${v}_f64" --steps 20 --warmup 5 --transforms 1
+        prof "${v}_f32" --steps 20 --warmup 5 --transforms 1 --precision single
+        prof "${v}_r2c512" --steps 10 --warmup 3 --transforms 1 --precision single --type r2c --size 512
+      done
+      unset SPFFT_AMD_LIBRARY ;;
     cmd:*) ncmd=$((ncmd + 1)); step cmd$ncmd 900 bash -c "${s#cmd:}" ;;
     *) echo "unknown suite $s"; exit 2 ;;
   esac
