@@ -71,15 +71,13 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(runs_, p.runs);
   upload(runOffsets_, p.stickRunOffsets);
   if (p.simpleSticks) upload(descs_, p.stickDescs);
-  std::vector<int> zRank(p.dimZ, 0);
+  zSeg_.assign(p.dimZ, 0);
   for (int r = 0; r < p.size; ++r)
-    for (int z = 0; z < p.planesPerRank[r]; ++z) zRank[p.planeOffsets[r] + z] = r;
-  upload(zRank_, zRank);
+    for (int z = 0; z < p.planesPerRank[r]; ++z) zSeg_[p.planeOffsets[r] + z] = r;
   std::vector<long long> sd(layout_.stickDispl.begin(), layout_.stickDispl.end());
-  std::vector<long long> ss(layout_.stickStride.begin(), layout_.stickStride.end());
-  upload(segDispl_, sd);
-  upload(segStride_, ss);
-  upload(segZOff_, p.planeOffsets);
+  segStride_.assign(layout_.stickStride.begin(), layout_.stickStride.end());
+  segZOff_.assign(p.planeOffsets.begin(), p.planeOffsets.end());
+  upload_ztab(zTab_, sd);
   upload(colOffsets_, p.colOffsets);
   upload(colY_, p.colY);
   std::vector<long long> cb(layout_.colEntryBase.begin(), layout_.colEntryBase.end());
@@ -119,7 +117,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
       // read it), so the exchange skips it instead of copying it on the device
       std::vector<long long> sdl(sd);
       sdl[p.rank] = slab_offset() + layout_.slabDispl[p.rank];
-      upload(segDispl_, sdl);
+      upload_ztab(zTab_, sdl);
       bwdSendCounts_[p.rank] = bwdRecvCounts_[p.rank] = 0;
     }
     // Exchange pipelining over plane chunks (build_chunk_plan): chunk k's
@@ -303,10 +301,10 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
       c.sc[me] = c.rc[me] = 0;
     }
   }
-  upload(zRank_, zSeg);
-  upload(segDispl_, segDispl);
-  upload(segStride_, segStride);
-  upload(segZOff_, segZOff);
+  zSeg_ = zSeg;
+  segStride_ = segStride;
+  segZOff_ = segZOff;
+  upload_ztab(zTab_, segDispl);
   exchChunks_ = K;
   commStream_.reset(new GpuStream(true));
   chunkEvents_.clear();
@@ -314,6 +312,21 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
   commDone_.reset(new GpuEvent());
   zDone_.reset(new GpuEvent());
   return true;
+}
+
+// Device table of the z stage's exchange segments: per plane z its segment's
+// (segDispl - segZOff + z, segStride), so (stick s, plane z) is one entry away.
+template <typename T>
+void GpuExecutor<T>::upload_ztab(std::unique_ptr<DeviceBuffer>& dst,
+                                 const std::vector<long long>& segDispl) {
+  const int Z = plan_->dimZ;
+  std::vector<long long> tab(2 * static_cast<std::size_t>(Z));
+  for (int z = 0; z < Z; ++z) {
+    const int v = zSeg_[z];
+    tab[2 * z] = segDispl[v] - segZOff_[v] + z;
+    tab[2 * z + 1] = segStride_[v];
+  }
+  upload(dst, tab);
 }
 
 // Element offset (exchange element type) from the stick-side buffer to the
@@ -383,7 +396,7 @@ void GpuExecutor<T>::build_peer_tables() {
     const i64 displ = layout_.buffered ? me * block : sticksBefore * p.planesPerRank[r];
     seg[r] = elem_offset(dc.peer_buffer(r, GridImpl<T>::kSlabSide), stick) + displ;
   }
-  upload(segDisplRemote_, seg);
+  upload_ztab(zTabRemote_, seg);  // peer writes never chunk: per-rank segments
   // forward: column entries of rank r's sticks land in r's stick side, block "from me"
   std::vector<long long> cb(p.colY.size());
   std::vector<long long> base(P);
@@ -685,10 +698,7 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
   a.desc = descs_ ? descs_->data<StickDesc>() : nullptr;
   a.single = p.size == 1 ? 1 : 0;
   a.stickStride = layout_.stickStride[0];
-  a.zRank = zRank_ ? zRank_->data<int>() : nullptr;
-  a.segDispl = segDispl_ ? segDispl_->data<long long>() : nullptr;
-  a.segStride = segStride_ ? segStride_->data<long long>() : nullptr;
-  a.segZOff = segZOff_ ? segZOff_->data<int>() : nullptr;
+  a.zTab = zTab_ ? zTab_->data<long long>() : nullptr;
   return a;
 }
 
@@ -778,7 +788,7 @@ void GpuExecutor<T>::backward_z(const T* input) {
   if (peerWrites_) {
     // the z stage stores straight into the peers' slab sides
     grid_->device_comm().prepare_write(GridImpl<T>::kSlabSide, stream_);
-    a.segDispl = segDisplRemote_->data<long long>();
+    a.zTab = zTabRemote_->data<long long>();
     a.remote = 1;
   }
   if (longZ_ && floatExchange_)

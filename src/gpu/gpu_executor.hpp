@@ -141,7 +141,14 @@ private:
   std::vector<GraphEntry> graphs_;
 
   // device tables
-  std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_, zRank_, segDispl_, segStride_, segZOff_;
+  std::unique_ptr<DeviceBuffer> runs_, runOffsets_, descs_;
+  // exchange segments of the z stage: segment v holds planes [segZOff, +n) of
+  // its sticks at segDispl[v] + s * segStride[v]; the device table (ZArgs::zTab)
+  // has one (base, stride) entry per plane
+  std::vector<int> zSeg_, segZOff_;
+  std::vector<long long> segStride_;
+  std::unique_ptr<DeviceBuffer> zTab_, zTabRemote_;
+  void upload_ztab(std::unique_ptr<DeviceBuffer>& dst, const std::vector<long long>& segDispl);
   std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
   // per-column run descriptors of the y stage (YArgs::colDesc), one per colBase
   // table in use; null when some column needs more than kColRuns runs.
@@ -167,7 +174,7 @@ private:
   // place on the slab side instead of being copied (SPFFT_LOCAL_DIRECT=0 copies)
   bool localDirect_ = false;
   long long slab_offset() const;
-  std::unique_ptr<DeviceBuffer> segDisplRemote_, colBaseRemote_;
+  std::unique_ptr<DeviceBuffer> colBaseRemote_;
   long long peerOffsetRange_[2] = {0, 0};  // min / max remote base (SPFFT_LOG)
 
   // Pipelined exchange (RCCL / loopback data planes, compact layout): every

@@ -42,10 +42,9 @@ struct ZArgs {
   const StickDesc* desc;     // non-null when every stick is simple (fast path)
   int single;                // 1: exchange side is the plain [S][stickStride] array
   long long stickStride;     // element stride between sticks when single
-  const int* zRank;          // n entries: rank owning plane z
-  const long long* segDispl; // per rank
-  const long long* segStride;
-  const int* segZOff;
+  // otherwise, per plane z two entries: (base, stride) of its exchange segment,
+  // element (stick s, plane z) at base + s * stride (base includes z)
+  const long long* zTab;
   int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
   BatchPtrs batch;
 };

@@ -416,18 +416,40 @@ __device__ __forceinline__ void release_remote(int remote) {
   if (remote) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
-__device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
-  if (a.single) return static_cast<long long>(s) * a.stickStride + pos;
-  const int r = a.zRank[pos];
-  return a.segDispl[r] + static_cast<long long>(s) * a.segStride[r] + (pos - a.segZOff[r]);
-}
-
 // A workgroup-uniform value materialised in a scalar register at this point:
 // the compiler may not sink its (scalar) load into later branches.
 __device__ __forceinline__ int pin_uniform(int v) {
   v = __builtin_amdgcn_readfirstlane(v);
   asm volatile("" : "+s"(v));
   return v;
+}
+
+__device__ __forceinline__ long long pin_uniform64(long long v) {
+  int lo = pin_uniform(static_cast<int>(v)), hi = pin_uniform(static_cast<int>(v >> 32));
+  return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+}
+
+// Exchange-side element of (stick s, plane pos): the plain stick array of a
+// single rank, else the plane's segment (one 16-byte table entry per plane:
+// no dependent loads). The arguments are pinned in scalar registers once per
+// kernel (read through ZArgs per element, their scalar loads were sunk into
+// every element's branch and waited out there).
+struct SegMap {
+  int single;
+  long long stride;
+  const long long* tab;
+  __device__ explicit SegMap(const ZArgs& a)
+      : single(pin_uniform(a.single)), stride(pin_uniform64(a.stickStride)), tab(a.zTab) {}
+  __device__ long long at(int s, int pos) const {
+    if (single) return static_cast<long long>(s) * stride + pos;
+    using V = long long __attribute__((ext_vector_type(2)));
+    const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
+    return t.x + static_cast<long long>(s) * t.y;
+  }
+};
+
+__device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
+  return SegMap(a).at(s, pos);
 }
 
 #define SPFFT_LDS_DECL(T)                                         \
@@ -580,6 +602,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, values, out);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
+  const SegMap seg(a);
   zero_lds(lds, eng.input_elems());
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
@@ -619,7 +642,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   if (a.zeroStick >= s0 && a.zeroStick < s0 + B) hermitian_lines(eng, lds, a.zeroStick - s0, 1, a.n);
   eng.lds_to_global(lds, tw, [&](int b, int pos, cx<T> v) {
     const int s = s0 + b;
-    if (s < a.numSticks) st_stream(&out[seg_index(a, s, pos)], cvt<typename BT::value_type>(v));
+    if (s < a.numSticks) st_stream(&out[seg.at(s, pos)], cvt<typename BT::value_type>(v));
   });
   release_remote(a.remote);
 }
@@ -632,10 +655,11 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
+  const SegMap seg(a);
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
-    return cvt<T>(ld_stream(&in[seg_index(a, s, pos)]));
+    return cvt<T>(ld_stream(&in[seg.at(s, pos)]));
   });
   // compress (+ scaling)
   RunTable tab;
@@ -688,8 +712,9 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
+  const SegMap seg(a);
   auto store = [&](int b, int pos, cx<T> v) {
-    if (b < nl) st_stream(&out[seg_index(a, s0 + b, pos)], cvt<typename BT::value_type>(v));
+    if (b < nl) st_stream(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -752,6 +777,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
+  const SegMap seg(a);
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
     // LDS round trip (69.6 -> 65.0 us at 256^3, profiles/r1_s14/zdesc_ab/
@@ -764,7 +790,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (lb < nl) q = a.desc[s0 + lb];
     eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
       if (b >= nl) return czero<T>();
-      return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
+      return cvt<T>(ld_stream(&in[seg.at(s0 + b, pos)]));
     }, [&](int b, int pos, cx<T> v) {
       assert(b == lb);
       if (b >= nl) return;
@@ -777,7 +803,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     __syncthreads();
     eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
       if (b >= nl) return czero<T>();
-      return cvt<T>(ld_stream(&in[seg_index(a, s0 + b, pos)]));
+      return cvt<T>(ld_stream(&in[seg.at(s0 + b, pos)]));
     }, [&](int b, int pos, cx<T> v) {
       if (b >= nl) return;
       const StickDesc& q = d[b];
@@ -1158,9 +1184,12 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (R2C) return mk<T>(ld_stream_real(&static_cast<const T*>(space)[row + pos]), T(0));
     return ld_stream(&static_cast<const cx<T>*>(space)[row + pos]);
   };
+  // arguments of the per-element stores pinned in scalar registers (see x_backward_kernel)
+  const int rowStride = pin_uniform(static_cast<int>(a.interStride)), nFreq = pin_uniform(a.nFreq);
+  const int dense = pin_uniform(x_dense(a) ? 1 : 0);
   auto store = [&](int b, int pos, cx<T> v) {
-    const int c = xcol_of(a, xCol, pos);
-    if (c >= 0 && b < yl) st_inter(&dst[inter_row(a, c) + b], v);
+    const int c = dense ? (pos < nFreq ? pos : -1) : xCol[pos];
+    if (c >= 0 && b < yl) st_inter(&dst[c * rowStride + b], v);
   };
 #if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
