@@ -788,14 +788,19 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const int lb = Eng::F::lane_line();
     StickDesc q{};
     if (lb < nl) q = a.desc[s0 + lb];
+    const int z0 = q.z0, len0 = lb < nl ? q.len0 : 0, z1 = q.z1, len1 = lb < nl ? q.count - q.len0 : 0;
+    cx<T>* vals = values + q.valueStart;
     eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
       if (b >= nl) return czero<T>();
       return cvt<T>(ld_stream(&in[seg.at(s0 + b, pos)]));
     }, [&](int b, int pos, cx<T> v) {
       assert(b == lb);
-      if (b >= nl) return;
-      const int j = desc_offset(q, pos);
-      if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
+      // branch-free value offset (as in the backward kernel); one predicated store
+      const unsigned j0 = static_cast<unsigned>(pos - z0), j1 = static_cast<unsigned>(pos - z1);
+      const bool in0 = j0 < static_cast<unsigned>(len0);
+      const bool in1 = j1 < static_cast<unsigned>(len1);
+      const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
+      if (in0 || in1) st_values(&vals[j], spfft::scale(v, scale));
     });
   } else {
     StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
