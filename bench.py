@@ -51,10 +51,14 @@ def parse():
                     help="independent transforms per step, run with multi_transform_backward/"
                          "forward on one stream each (the reference benchmark's -m): one "
                          "transform's all-to-all overlaps the others' FFT kernels")
-    ap.add_argument("--streams", default="per-transform", choices=["per-transform", "one"],
+    ap.add_argument("--streams", default="auto", choices=["auto", "per-transform", "one"],
                     help="with --sync stream and T > 1: one stream per transform (their kernels "
-                         "overlap), or all transforms on torch's current stream (identical "
-                         "transforms then run batched, one launch per stage for up to 8)")
+                         "and exchanges overlap), or all transforms on torch's current stream "
+                         "(identical single-GPU transforms then run batched, one launch per "
+                         "stage for up to 8). auto: one stream on 1 GPU (batched launches "
+                         "measured +2%% over 4 streams at 256^3, profiles/r3/t4_streams.txt), "
+                         "per-transform streams on N > 1 GPUs (one transform's all-to-all "
+                         "overlaps the others' kernels; distributed plans do not batch)")
     ap.add_argument("--timing", action="store_true", help="print the native timing tree")
     ap.add_argument("--check", action="store_true",
                     help="after timing: round-trip error on every rank and, on one rank, the "
@@ -151,6 +155,8 @@ def main():
     grid, t = grids[0], ts[0]
 
     plane = grid.data_plane if world > 1 else "none"
+    if a.streams == "auto":
+        a.streams = "one" if world == 1 else "per-transform"
     streams = []
     if a.sync == "stream":
         if T == 1 or a.streams == "one":
