@@ -573,6 +573,45 @@ __device__ __forceinline__ int find_run(const RunTable& t, int idx) {
   return lo;
 }
 
+// Exchange-side addressing of the z stage kernels, by plan kind (template
+// argument, chosen at launch): a single rank's plain stick array (pinned stride,
+// pure arithmetic), or, on distributed plans, the per-plane segment table
+// staged in LDS once per workgroup. Read from global memory per element, the
+// table entry's wait (s_waitcnt vmcnt) also waited out every data load the lane
+// had issued before it; LDS reads count separately (lgkmcnt) and, with no
+// branch per element, issue back to back.
+template <bool Single>
+struct ZSeg {
+  long long stride = 0;
+  const long long* tab = nullptr;  // LDS: (base, stride) per plane
+  __device__ ZSeg(const ZArgs& a, char* ldsTab, int n) {
+    if constexpr (Single) {
+      stride = pin_uniform64(a.stickStride);
+    } else {
+      long long* t = reinterpret_cast<long long*>(ldsTab);
+      for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) t[i] = a.zTab[i];
+      __syncthreads();
+      tab = t;
+    }
+  }
+  __device__ long long at(int s, int pos) const {
+    if constexpr (Single) {
+      return static_cast<long long>(s) * stride + pos;
+    } else {
+      using V = long long __attribute__((ext_vector_type(2)));
+      const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
+      return t.x + static_cast<long long>(s) * t.y;
+    }
+  }
+};
+// LDS offset of ZSeg's table behind the FFT lines and the desc / run table
+__host__ __device__ constexpr std::size_t zseg_lds_offset(std::size_t fftBytes, int lines) {
+  return (fftBytes + run_table_bytes(lines) + 15) / 16 * 16;
+}
+inline std::size_t zseg_lds_bytes(const ZArgs& a) {
+  return a.single ? 0 : std::size_t(2) * a.n * sizeof(long long) + 16;
+}
+
 // Workgroup -> tile mapping: the dispatcher deals consecutive workgroups
 // round-robin to the 8 XCDs. An XCD-contiguous remap was measured slower on
 // MI355X at 256^3 (x/y stages 3-6 us, bench -4.5%, profiles/r2_s1/shape_ab.txt):
@@ -594,7 +633,7 @@ __device__ __forceinline__ int block_tile_x() { return blockIdx.x; }
   }
 
 // ---------------------------------------------------------------- z stage
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Single>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values, BT* __restrict__ out,
                       const cx<T>* __restrict__ tw) {
@@ -602,7 +641,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, values, out);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
-  const SegMap seg(a);
+  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   zero_lds(lds, eng.input_elems());
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
@@ -647,7 +686,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   release_remote(a.remote);
 }
 
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Single>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                      T scale, const cx<T>* __restrict__ tw) {
@@ -655,7 +694,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
-  const SegMap seg(a);
+  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
@@ -702,7 +741,7 @@ __device__ __forceinline__ int desc_offset(const StickDesc& q, int z) {
   return -1;
 }
 
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Single>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
@@ -712,7 +751,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
-  const SegMap seg(a);
+  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   auto store = [&](int b, int pos, cx<T> v) {
     if (b < nl) st_stream(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
@@ -768,7 +807,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   release_remote(a.remote);
 }
 
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Single>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                           T scale, const cx<T>* __restrict__ tw) {
@@ -777,7 +816,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
-  const SegMap seg(a);
+  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
     // LDS round trip (69.6 -> 65.0 us at 256^3, profiles/r1_s14/zdesc_ab/
@@ -791,8 +830,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const int z0 = q.z0, len0 = lb < nl ? q.len0 : 0, z1 = q.z1, len1 = lb < nl ? q.count - q.len0 : 0;
     cx<T>* vals = values + q.valueStart;
     eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
-      if (b >= nl) return czero<T>();
-      return cvt<T>(ld_stream(&in[seg.at(s0 + b, pos)]));
+      // unconditional load (lanes past the last stick read a valid one): no
+      // branch per element, so the loads (and segment-table reads) issue back to back
+      const cx<T> v = cvt<T>(ld_stream(&in[seg.at(s0 + min(b, nl - 1), pos)]));
+      return b < nl ? v : czero<T>();
     }, [&](int b, int pos, cx<T> v) {
       assert(b == lb);
       // branch-free value offset (as in the backward kernel); one predicated store
