@@ -156,11 +156,29 @@ __device__ __forceinline__ void scatter_from_lds(const cx<T>* lds, int total, Sr
 // LDS -> global copy-out of a stage kernel: the run-time engines batch their LDS
 // reads (scatter_from_lds, measured +5-7% at 100^3-240^3); the compile-time
 // engines keep the plain loop (batching measured 1-2% slower at 128^3-256^3).
+// A full tile of a compile-time engine (every line present) copies with a
+// fully unrolled loop of compile-time trip count E: its LDS reads issue back to
+// back instead of one read, wait and store per iteration.
+#ifndef SPFFT_STATIC_COPY
+#define SPFFT_STATIC_COPY 1
+#endif
 template <class Eng, typename T, class Src, class St>
 __device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, St st) {
   if constexpr (Eng::kBatchedCopy) {
     scatter_from_lds(lds, total, src, st);
   } else {
+    using F = typename Eng::F;
+    // (mixed-radix shapes can leave lanes idle: their tiles need not split evenly)
+    constexpr bool kEven = (F::B * Eng::kN) % F::NT == 0;
+    if (SPFFT_STATIC_COPY && kEven && total == F::B * Eng::kN) {
+      constexpr int kIters = kEven ? F::B * Eng::kN / F::NT : 1;
+      cx<T> v[kIters];
+#pragma unroll
+      for (int i = 0; i < kIters; ++i) v[i] = lds[src(static_cast<int>(threadIdx.x) + i * F::NT)];
+#pragma unroll
+      for (int i = 0; i < kIters; ++i) st(static_cast<int>(threadIdx.x) + i * F::NT, v[i]);
+      return;
+    }
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) st(idx, lds[src(idx)]);
   }
 }
