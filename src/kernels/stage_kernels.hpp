@@ -591,35 +591,34 @@ __device__ __forceinline__ int find_run(const RunTable& t, int idx) {
   return lo;
 }
 
-// Exchange-side addressing of the z stage kernels, by plan kind (template
-// argument, chosen at launch): a single rank's plain stick array (pinned stride,
-// pure arithmetic), or, on distributed plans, the per-plane segment table
-// staged in LDS once per workgroup. Read from global memory per element, the
-// table entry's wait (s_waitcnt vmcnt) also waited out every data load the lane
-// had issued before it; LDS reads count separately (lgkmcnt) and, with no
-// branch per element, issue back to back.
-template <bool Single>
+// Exchange-side addressing of the z stage kernels. A single rank's stick array
+// is pure arithmetic (stride pinned in scalar registers). Distributed plans
+// stage their per-plane segment table, (base, stride) per plane z (ZArgs::zTab),
+// in LDS once per workgroup: read from global memory per element, a table
+// entry's wait (s_waitcnt vmcnt) also waited out every data load the lane had
+// issued before it, while LDS reads count separately (lgkmcnt). Only
+// distributed launches reserve the table's LDS: at 256^3 fp64 its 4 KB cost
+// the z forward kernel a third of its workgroups per CU (66 -> 73 us), as did
+// computing a single rank's table in LDS. (A kernel template per plan kind
+// doubled the z kernels and tripled their compile time.)
 struct ZSeg {
-  long long stride = 0;
-  const long long* tab = nullptr;  // LDS: (base, stride) per plane
-  __device__ ZSeg(const ZArgs& a, char* ldsTab, int n) {
-    if constexpr (Single) {
-      stride = pin_uniform64(a.stickStride);
-    } else {
+  int single;
+  long long stride;
+  const long long* tab;  // LDS (distributed plans)
+  __device__ ZSeg(const ZArgs& a, char* ldsTab, int n)
+      : single(pin_uniform(a.single)), stride(pin_uniform64(a.stickStride)),
+        tab(reinterpret_cast<const long long*>(ldsTab)) {
+    if (!single) {
       long long* t = reinterpret_cast<long long*>(ldsTab);
       for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) t[i] = a.zTab[i];
       __syncthreads();
-      tab = t;
     }
   }
   __device__ long long at(int s, int pos) const {
-    if constexpr (Single) {
-      return static_cast<long long>(s) * stride + pos;
-    } else {
-      using V = long long __attribute__((ext_vector_type(2)));
-      const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
-      return t.x + static_cast<long long>(s) * t.y;
-    }
+    if (single) return static_cast<long long>(s) * stride + pos;
+    using V = long long __attribute__((ext_vector_type(2)));
+    const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
+    return t.x + static_cast<long long>(s) * t.y;
   }
 };
 // LDS offset of ZSeg's table behind the FFT lines and the desc / run table
@@ -651,7 +650,7 @@ __device__ __forceinline__ int block_tile_x() { return blockIdx.x; }
   }
 
 // ---------------------------------------------------------------- z stage
-template <class Eng, typename T, typename BT, bool Single>
+template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values, BT* __restrict__ out,
                       const cx<T>* __restrict__ tw) {
@@ -659,7 +658,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, values, out);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
-  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
+  const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   zero_lds(lds, eng.input_elems());
   RunTable tab;
   char* tableBase = reinterpret_cast<char*>(lds) + eng.lds_bytes();
@@ -704,7 +703,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   release_remote(a.remote);
 }
 
-template <class Eng, typename T, typename BT, bool Single>
+template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                      T scale, const cx<T>* __restrict__ tw) {
@@ -712,7 +711,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   SPFFT_BATCH_SELECT(a, in, values);
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
-  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
+  const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   eng.global_to_lds(lds, tw, [&](int b, int pos) -> cx<T> {
     const int s = s0 + b;
     if (s >= a.numSticks) return czero<T>();
@@ -759,7 +758,7 @@ __device__ __forceinline__ int desc_offset(const StickDesc& q, int z) {
   return -1;
 }
 
-template <class Eng, typename T, typename BT, bool Single>
+template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
@@ -769,7 +768,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
-  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
+  const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   auto store = [&](int b, int pos, cx<T> v) {
     if (b < nl) st_stream(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
@@ -825,7 +824,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   release_remote(a.remote);
 }
 
-template <class Eng, typename T, typename BT, bool Single>
+template <class Eng, typename T, typename BT>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                           T scale, const cx<T>* __restrict__ tw) {
@@ -834,7 +833,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int B = eng.lines();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
-  const ZSeg<Single> seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
+  const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   if constexpr (!Eng::kBatchedCopy) {
     // compile-time engines: the lane's own stick descriptor in registers, no
     // LDS round trip (69.6 -> 65.0 us at 256^3, profiles/r1_s14/zdesc_ab/

@@ -11,8 +11,7 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
   if (a.numSticks <= a.stickBegin) return;
   with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     using E = decltype(eng);
-    auto k = a.single ? (a.desc ? z_backward_desc_kernel<E, T, BT, true> : z_backward_kernel<E, T, BT, true>)
-                      : (a.desc ? z_backward_desc_kernel<E, T, BT, false> : z_backward_kernel<E, T, BT, false>);
+    auto k = a.desc ? z_backward_desc_kernel<E, T, BT> : z_backward_kernel<E, T, BT>;
     const std::size_t ldsTotal = zseg_lds_offset(lds, lines) + zseg_lds_bytes(a);
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,

@@ -11,8 +11,7 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
   if (a.numSticks <= a.stickBegin) return;
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     using E = decltype(eng);
-    auto k = a.single ? (a.desc ? z_forward_desc_kernel<E, T, BT, true> : z_forward_kernel<E, T, BT, true>)
-                      : (a.desc ? z_forward_desc_kernel<E, T, BT, false> : z_forward_kernel<E, T, BT, false>);
+    auto k = a.desc ? z_forward_desc_kernel<E, T, BT> : z_forward_kernel<E, T, BT>;
     const std::size_t ldsTotal = zseg_lds_offset(lds, lines) + zseg_lds_bytes(a);
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
