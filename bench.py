@@ -61,8 +61,11 @@ def parse():
                          "overlaps the others' kernels; distributed plans do not batch)")
     ap.add_argument("--timing", action="store_true", help="print the native timing tree")
     ap.add_argument("--check", action="store_true",
-                    help="after timing: round-trip error on every rank and, on one rank, the "
-                         "backward transform against the dense numpy oracle")
+                    help="also compare the backward transform against the dense numpy oracle "
+                         "(1 rank; the GPU round-trip check on every rank always runs)")
+    ap.add_argument("--profile-reps", type=int, default=5,
+                    help="backward+forward pairs of transform 0 timed per stage after the "
+                         "timed loop (0 = no stage profile)")
     ap.add_argument("--sync", default="stream", choices=["stream", "call"],
                     help="stream: transforms are stream-ordered on torch's current stream (no host "
                          "wait per call; the timed loop still ends with a device synchronize); "
@@ -71,31 +74,82 @@ def parse():
 
 
 def _check(a, sp, t, values, gidx, dims, ttype, world):
-    """Max relative error of the round trip (and of the backward vs numpy on 1 rank)."""
-    import numpy as np
+    """Backward vs the dense numpy oracle (1 rank, --check): max relative error."""
     import torch
     from spfft_amd.utils.oracle import dense_backward, max_rel_error
-    out = torch.empty_like(values)
     space = t.backward(values)
     torch.cuda.synchronize()
-    err = {}
-    if world == 1 and max(dims) <= 512:  # the dense numpy oracle (host memory, time)
-        ref = dense_backward(gidx, values.cpu().numpy(), dims,
-                             r2c=(ttype == sp.TransformType.R2C))
-        err["backward_vs_numpy"] = max_rel_error(space.cpu().numpy(), ref)
-    t.forward(None, output=out, scaling=sp.Scaling.FULL)
-    torch.cuda.synchronize()
-    if ttype == sp.TransformType.R2C:
-        # random R2C input is not hermitian on the x = 0 plane: compare the second
-        # round trip with the first (the round trip is a projection)
-        ref_rt = out.clone()
-        t.backward(ref_rt)
-        t.forward(None, output=out, scaling=sp.Scaling.FULL)
+    ref = dense_backward(gidx, values.cpu().numpy(), dims, r2c=(ttype == sp.TransformType.R2C))
+    return {"backward_vs_numpy": max_rel_error(space.cpu().numpy(), ref)}
+
+
+def _roundtrip_gpu(sp, ts, vals, outs, r2c):
+    """Round-trip error of every transform of this rank, computed on the GPU (no host
+    copies): backward + forward with full scaling must reproduce the input. Random
+    R2C input is not hermitian on the x = 0 plane, so R2C compares the second round
+    trip with the first (the round trip is a projection)."""
+    import torch
+    worst = 0.0
+    for t, v, o in zip(ts, vals, outs):
+        if v.numel() == 0:
+            continue
+        t.backward(v)
+        t.forward(None, output=o, scaling=sp.Scaling.FULL)
+        base = v
+        if r2c:
+            torch.cuda.synchronize()
+            base = o.clone()
+            t.backward(base)
+            t.forward(None, output=o, scaling=sp.Scaling.FULL)
         torch.cuda.synchronize()
-        err["roundtrip"] = max_rel_error(out.cpu().numpy(), ref_rt.cpu().numpy())
-    else:
-        err["roundtrip"] = max_rel_error(out.cpu().numpy(), values.cpu().numpy())
-    return err
+        scale = float(base.abs().max().item()) or 1.0
+        worst = max(worst, float((o - base).abs().max().item()) / scale)
+    return worst
+
+
+def _timing_node(tree, path):
+    nodes = tree.get("timings", [])
+    node = None
+    for name in path:
+        node = next((n for n in nodes if n["identifier"] == name), None)
+        if node is None:
+            return None
+        nodes = node.get("sub-timings", [])
+    return node
+
+
+def _stage_profile(sp, t, values, out, reps):
+    """Per-direction GPU stage times of ONE transform run alone (outside the timed
+    loop): hipEvent intervals at the stage boundaries on the transform's stream
+    (gpu/<direction>/<stage>) and, for pipelined exchanges, the span of the exchange
+    on the data plane's stream (exchange-span). Medians in milliseconds."""
+    import torch
+    sp.timing_reset()
+    sp.timing_enable(True)
+    for _ in range(reps):
+        t.backward(values)
+        t.forward(None, output=out)
+    torch.cuda.synchronize()
+    t.synchronize()  # completes the stage intervals
+    sp.timing_enable(False)
+    tree = sp.timing_json()
+    prof = {}
+    for direction in ("backward", "forward"):
+        node = _timing_node(tree, ["gpu", direction])
+        if node is None:
+            continue
+        prof[direction] = {c["identifier"]: 1e3 * c["median"] for c in node.get("sub-timings", [])}
+        prof[direction]["total"] = sum(v for k, v in prof[direction].items() if k != "exchange-span")
+    sp.timing_reset()
+    return prof
+
+
+def _metric(n, ttype, cutoff, single):
+    headline = "3D C2C transforms/sec, 256^3 spherical cutoff, 1/2/4/8 MI355X"
+    if n == 256 and ttype == "c2c" and cutoff == 0.5 and not single:
+        return headline  # BASELINE.json's metric string
+    prec = "fp32" if single else "fp64"
+    return f"3D {ttype.upper()} {prec} transforms/sec, {n}^3 spherical cutoff r={cutoff}*N, MI355X"
 
 
 def main():
@@ -141,11 +195,11 @@ def main():
         # every transform owns its grid (multi_transform rejects shared grids)
         if world == 1:
             g = GridCls(n, n, n, n * n, sp.ProcessingUnit.GPU, 1)
-            return g, g.create_transform(sp.ProcessingUnit.GPU, ttype, n, n, n, n, gidx), gidx
+            return g, g.create_transform(sp.ProcessingUnit.GPU, ttype, n, n, n, n, gidx), gidx, n
         from spfft_amd.parallel import TorchDistComm, make_distributed
         setup = make_distributed(TorchDistComm(), dims, gidx, processing_unit=sp.ProcessingUnit.GPU,
                                  transform_type=ttype, exchange_type=exch, single=single)
-        return setup.grid, setup.transform, setup.indices
+        return setup.grid, setup.transform, setup.indices, setup.z_length
 
     T = max(1, a.transforms)
     made = [make_transform() for _ in range(T)]
@@ -204,15 +258,45 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    check = None
-    if a.check:
-        check = _check(a, sp, t, values, gidx, dims, ttype, world)
-        if dist is not None:
-            # every rank's round trip counts: rank 0 reports the worst one
-            e = torch.tensor([check["roundtrip"]], dtype=torch.float64)
-            dist.all_reduce(e, op=dist.ReduceOp.MAX)
-            check["roundtrip"] = float(e.item())
-            check["ranks_checked"] = world
+    if a.timing:
+        for tr in ts:  # completes the GPU stage intervals (gpu/<direction>/<stage>)
+            tr.synchronize()
+        if rank == 0:
+            print(sp.timing_report(), file=sys.stderr)
+        sp.timing_enable(False)
+    # Self-check outside the timed region, on every rank and every transform,
+    # on the GPU: a multi-GPU record carries its own proof that the exchange
+    # moved the right bytes. The worst rank is reported.
+    check = {"roundtrip": _roundtrip_gpu(sp, ts, vals, outs, ttype == sp.TransformType.R2C),
+             "ranks_checked": world, "transforms_checked": T,
+             "method": "max |forward(backward(v)) - v| / max |v| with full scaling, on the GPU"}
+    if dist is not None:
+        e = torch.tensor([check["roundtrip"]], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        check["roundtrip"] = float(e.item())
+    check["tolerance"] = 1e-4 if (single or "Float" in a.exchange) else 1e-10
+    check["ok"] = check["roundtrip"] < check["tolerance"]
+    if a.check and world == 1:
+        check.update(_check(a, sp, t, values, gidx, dims, ttype, world))
+    # per-direction stage times of transform 0 alone, and the exchange rate
+    stages = _stage_profile(sp, t, values, out, a.profile_reps) if a.profile_reps > 0 else {}
+    exch = None
+    if world > 1 and stages:
+        eb = (8 if single or "Float" in a.exchange else 16)
+        loc = np.asarray(local).reshape(-1, 3).astype(np.int64)
+        local_sticks = int(np.unique((loc[:, 0] % n) * n + (loc[:, 1] % n)).size) if len(loc) else 0
+        z_len = made[0][3]
+        sent = local_sticks * (n - z_len) * eb  # compact layout: every non-local plane leaves
+        ms = {}
+        for d in ("backward", "forward"):
+            st = stages.get(d, {})
+            ms[d] = st.get("exchange-span", st.get("exchange"))
+        exch = {"bytes_sent_per_rank": sent,
+                "ms": ms,
+                "GBps_per_rank": {d: (sent / (v * 1e-3) / 1e9 if v else None) for d, v in ms.items()}}
+        e = torch.tensor([float(sent)], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        exch["max_bytes_sent_per_rank"] = float(e.item())
     # ranks that share a device (rehearsal on a small box) are not a multi-GPU
     # measurement: record how many distinct devices the job really used
     n_devices = min(world, ndev)
@@ -228,14 +312,9 @@ def main():
     # multi-transform overlap into the per-transform speed-up
     ref_rate = REF_FFT_ONLY_256_BY_T.get(T) if (headline and world == 1) else None
     vs_baseline = rate / ref_rate if ref_rate else None
-    if a.timing:
-        for tr in ts:  # completes the GPU stage intervals (gpu/<direction>/<stage>)
-            tr.synchronize()
     if rank == 0:
-        if a.timing:
-            print(sp.timing_report(), file=sys.stderr)
         rec = {
-            "metric": "3D C2C transforms/sec, 256^3 spherical cutoff, 1/2/4/8 MI355X",
+            "metric": _metric(n, a.type, a.cutoff, single),
             "value": rate,
             "unit": "transforms/s",
             "n_gpus": world,
@@ -264,7 +343,12 @@ def main():
                 "shared_device": n_devices < world,
                 "sync": a.sync,
                 "streams": a.streams if T > 1 else "one",
+                "library_streams": sp.library_streams(),
                 "check_error": check,
+                "stage_ms": stages,
+                "stage_ms_basis": (f"transform 0 alone, median of {a.profile_reps} backward+forward "
+                                   "pairs after the timed loop (hipEvent stage marks)" if stages else None),
+                "exchange": exch,
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),
             },

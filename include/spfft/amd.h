@@ -71,6 +71,10 @@ SPFFT_EXPORT SpfftError spfft_amd_float_grid_device_bytes(SpfftFloatGrid grid,
  * communicators have the same members on the same devices share one
  * (SPFFT_RCCL_SHARE=0: one per grid). */
 SPFFT_EXPORT SpfftError spfft_amd_rccl_communicators(int* count);
+/* HIP streams the library currently owns: private transform streams (created
+ * on a transform's first call unless it was given a stream before) and RCCL
+ * channel streams (one per shared communicator). */
+SPFFT_EXPORT SpfftError spfft_amd_library_streams(int* count);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 

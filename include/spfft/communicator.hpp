@@ -60,6 +60,15 @@ public:
 
   /* True for the in-process local group (GPU data plane uses peer copies instead of RCCL). */
   virtual bool is_local_group() const { return false; }
+
+  /* Ordering domain of the GPU data plane. Grids whose communicators have the
+   * same members and the same domain on every rank share one RCCL communicator,
+   * whose exchanges run in host call order (the order every rank issues them
+   * in, transforms being collective on their communicator). MPI: the user
+   * communicator the grid was built from, so grids on distinct MPI
+   * communicators, which MPI_THREAD_MULTIPLE lets threads drive concurrently,
+   * never share one. 0 (default) = members only. */
+  virtual unsigned long long channel_domain() const { return 0; }
 };
 
 /* Creates `size` communicators forming one in-process group; element r has rank r.

@@ -44,3 +44,16 @@ def rccl_communicators() -> int:
     if rc != 0:
         raise RuntimeError(f"spfft_amd_rccl_communicators failed ({rc})")
     return n.value
+
+
+def library_streams() -> int:
+    """HIP streams the library currently owns (private transform streams, created on a
+    transform's first call unless it was given a stream first, and RCCL channel
+    streams)."""
+    import ctypes
+    from .ops._lib import lib
+    n = ctypes.c_int()
+    rc = lib().spfft_amd_library_streams(ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"spfft_amd_library_streams failed ({rc})")
+    return n.value

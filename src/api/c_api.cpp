@@ -7,6 +7,7 @@
 
 #include "api/transform_impl.hpp"
 #include "comm/callback_comm.hpp"
+#include "gpu/gpu_runtime.hpp"
 #include "core/common.hpp"
 #include "core/timing.hpp"
 #include "gpu/device_comm.hpp"
@@ -376,6 +377,12 @@ SpfftError spfft_amd_float_grid_device_bytes(SpfftFloatGrid grid, unsigned long 
 SpfftError spfft_amd_rccl_communicators(int* count) {
   if (!count) return SPFFT_INVALID_PARAMETER_ERROR;
   *count = spfft::DeviceComm::rccl_channels_created();
+  return SPFFT_SUCCESS;
+}
+
+SpfftError spfft_amd_library_streams(int* count) {
+  if (!count) return SPFFT_INVALID_PARAMETER_ERROR;
+  *count = spfft::GpuStream::live();
   return SPFFT_SUCCESS;
 }
 

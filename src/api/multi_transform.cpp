@@ -36,6 +36,8 @@ std::vector<bool> run_batches(const std::vector<TransformImpl<T>*>& ts, Eligible
                               Run run) {
   const int n = static_cast<int>(ts.size());
   std::vector<bool> done(n, false);
+  for (auto* t : ts)
+    if (t->is_gpu()) t->gpu()->ensure_stream();  // the stream comparisons below need them
   auto ok = [&](int j) {
     return !done[j] && ts[j]->is_gpu() && ts[j]->gpu()->batchable() && eligible(j);
   };

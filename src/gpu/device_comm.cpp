@@ -27,13 +27,42 @@ namespace spfft {
 DeviceComm::~DeviceComm() = default;
 
 double comm_timeout_seconds() {
-  // default 120 s: a dead or missing peer becomes an MPIError instead of a hang;
-  // SPFFT_COMM_TIMEOUT=0 waits forever
+  // default 0 = no limit: waiting for a slower rank is not an error (MPI
+  // semantics); failures are still detected through the data plane's
+  // asynchronous error state while the host waits
   static const double t = [] {
     const char* e = std::getenv("SPFFT_COMM_TIMEOUT");
-    return e && *e ? std::max(0.0, std::atof(e)) : 120.0;
+    return e && *e ? std::max(0.0, std::atof(e)) : 0.0;
   }();
   return t;
+}
+
+double comm_init_timeout_seconds() {
+  const double t = comm_timeout_seconds();
+  return t > 0 ? t : 300.0;
+}
+
+void append_alltoallv(std::vector<Transfer>& out, int me, int P, const std::int64_t* sc,
+                      const std::int64_t* sd, const std::int64_t* rc, const std::int64_t* rd) {
+  // the own block never leaves the GPU
+  if (sc[me] != rc[me]) throw MPIError();
+  if (sc[me] > 0) out.push_back({Transfer::kLocal, me, sd[me], rd[me], sc[me]});
+  for (int k = 1; k < P; ++k) {
+    const int to = (me + k) % P;
+    const int from = (me - k + P) % P;
+    if (sc[to] > 0) out.push_back({Transfer::kSend, to, sd[to], 0, sc[to]});
+    if (rc[from] > 0) out.push_back({Transfer::kRecv, from, rd[from], 0, rc[from]});
+  }
+}
+
+void DeviceComm::alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd,
+                           void* recv, const std::int64_t* rc, const std::int64_t* rd,
+                           hipStream_t stream) {
+  std::vector<Transfer> xs;
+  xs.reserve(2 * 8);
+  // (rank and size come from the plane: the counts have one entry per rank)
+  append_alltoallv(xs, plane_rank(), plane_size(), sc, sd, rc, rd);
+  exchange(send, recv, xs, stream, nullptr);
 }
 
 namespace {
@@ -41,8 +70,9 @@ namespace {
 // ------------------------------------------------------------- RCCL channel
 // One RCCL communicator plus the stream that carries every exchange issued on
 // it. Grids of one process whose communicators have the same members on the
-// same devices share one channel (DeviceComm::create): `bench.py --gpus 8`
-// with 4 transforms builds one RCCL communicator per rank, not four, and every
+// same devices and the same ordering domain (Communicator::channel_domain)
+// share one channel (DeviceComm::create): `bench.py --gpus 8` with 4
+// transforms builds one RCCL communicator per rank, not four, and every
 // exchange of the process runs on one stream in host call order, the order
 // every rank issues them in (transforms are collective). Concurrent kernels of
 // several communicators, whose relative order can differ between ranks, are
@@ -62,14 +92,14 @@ struct NcclChannel {
   bool ok() const { return comm != nullptr; }
 
   // Non-blocking communicator calls return ncclInProgress while RCCL works in
-  // the background: poll until done, abort past the deadline (a rank that
+  // the background: poll until done, give up past the deadline (a rank that
   // never arrives cannot leave the others inside RCCL).
   ncclResult_t settle(ncclResult_t r, double seconds) {
     using clock = std::chrono::steady_clock;
     const auto t0 = clock::now();
     while (r == ncclInProgress) {
       if (seconds > 0 && std::chrono::duration<double>(clock::now() - t0).count() > seconds) {
-        detail = "RCCL: no progress within SPFFT_COMM_TIMEOUT = " + std::to_string(seconds) + " s";
+        detail = "RCCL: no progress within " + std::to_string(seconds) + " s";
         return ncclInProgress;
       }
       std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -109,7 +139,7 @@ struct NcclChannel {
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
     ncclResult_t r = ncclCommInitRankConfig(&comm, size, root.id, rank, &cfg);
-    if (r == ncclInProgress || r == ncclSuccess) r = settle(r, comm_timeout_seconds());
+    if (r == ncclInProgress || r == ncclSuccess) r = settle(r, comm_init_timeout_seconds());
     if (r != ncclSuccess) {
       if (detail.empty()) detail = std::string("RCCL: ncclCommInitRankConfig: ") + ncclGetErrorString(r);
       if (comm) (void)ncclCommAbort(comm);
@@ -127,11 +157,16 @@ struct NcclChannel {
       throw MPIError();
     }
   }
+  // A failed call leaves the communicator (and an open group) in an undefined
+  // state: the channel is aborted before the error propagates, so later
+  // exchanges on it fail fast instead of reusing it. Caller holds `m`.
   void nccl_check(ncclResult_t r, const char* what) {
-    if (r == ncclInProgress) r = settle(r, comm_timeout_seconds());
+    if (r == ncclInProgress) r = settle(r, comm_init_timeout_seconds());
     if (r != ncclSuccess) {
-      set_error_detail(std::string("RCCL ") + what + ": " + ncclGetErrorString(r) + " " +
+      set_error_detail(std::string("RCCL ") + what + ": " +
+                       (r == ncclInProgress ? std::string("no progress") : ncclGetErrorString(r)) + " " +
                        (detail.empty() ? ncclGetLastError(comm) : detail));
+      abort_locked();
       throw MPIError();
     }
   }
@@ -142,23 +177,44 @@ struct NcclChannel {
     std::size_t bytes;
     int peer;
   };
-  // Enqueues the transfers after the work queued so far on `caller`; `caller`
-  // continues once every block has arrived.
-  void run(const std::vector<Xfer>& xs, hipStream_t caller) {
+  // Enqueues the transfers. sync == nullptr: after the work queued so far on
+  // `caller`, which continues once every block has arrived (one event pair).
+  // Otherwise on the channel stream after sync->ready, recording sync->done.
+  // `local` copies run on the same stream, ahead of the group.
+  void run(const std::vector<Xfer>& xs, const std::vector<Xfer>& local, hipStream_t caller,
+           const ExchangeSync* sync) {
     std::lock_guard<std::mutex> lock(m);
     check_usable();
     DeviceGuard guard(device);
     hipStream_t cs = stream->get();
-    in->record(caller);
-    in->wait_on(cs);
-    nccl_check(ncclGroupStart(), "ncclGroupStart");
-    for (const Xfer& x : xs) {
-      if (x.send) nccl_check(ncclSend(x.send, x.bytes, ncclChar, x.peer, comm, cs), "ncclSend");
-      if (x.recv) nccl_check(ncclRecv(x.recv, x.bytes, ncclChar, x.peer, comm, cs), "ncclRecv");
+    if (sync) {
+      if (sync->ready) gpu_check(hipStreamWaitEvent(cs, sync->ready, 0), "hipStreamWaitEvent");
+      if (sync->begin) gpu_check(hipEventRecord(sync->begin, cs), "hipEventRecord");
+    } else {
+      in->record(caller);
+      in->wait_on(cs);
     }
-    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-    out->record(cs);
-    out->wait_on(caller);
+    for (const Xfer& x : local)
+      gpu_check(hipMemcpyAsync(x.recv, x.send, x.bytes, hipMemcpyDeviceToDevice, cs), "hipMemcpyAsync");
+    if (!xs.empty()) {
+      nccl_check(ncclGroupStart(), "ncclGroupStart");
+      for (const Xfer& x : xs) {
+        const ncclResult_t r = x.send ? ncclSend(x.send, x.bytes, ncclChar, x.peer, comm, cs)
+                                      : ncclRecv(x.recv, x.bytes, ncclChar, x.peer, comm, cs);
+        if (r != ncclSuccess && r != ncclInProgress) {
+          (void)ncclGroupEnd();
+          nccl_check(r, x.send ? "ncclSend" : "ncclRecv");
+        }
+      }
+      nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+    if (sync) {
+      if (sync->done) gpu_check(hipEventRecord(sync->done, cs), "hipEventRecord");
+      if (sync->end) gpu_check(hipEventRecord(sync->end, cs), "hipEventRecord");
+    } else {
+      out->record(cs);
+      out->wait_on(caller);
+    }
   }
 
   bool healthy(std::string* why) {
@@ -172,17 +228,20 @@ struct NcclChannel {
     if (why) *why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
     return false;
   }
-  void abort() {
-    std::lock_guard<std::mutex> lock(m);
+  void abort_locked() {
     if (aborted || !comm) return;
     aborted = true;
     (void)ncclCommAbort(comm);
     comm = nullptr;
   }
+  void abort() {
+    std::lock_guard<std::mutex> lock(m);
+    abort_locked();
+  }
 };
 
 // Process-wide channel registry, keyed by the member list (host, pid, device of
-// every rank, in rank order) and the device.
+// every rank, in rank order), the ordering domain and the device.
 std::mutex gChannelMutex;
 std::map<std::string, std::weak_ptr<NcclChannel>>& channel_registry() {
   static auto* r = new std::map<std::string, std::weak_ptr<NcclChannel>>();  // outlives atexit
@@ -202,31 +261,35 @@ class RcclDeviceComm : public DeviceComm {
 public:
   explicit RcclDeviceComm(std::shared_ptr<NcclChannel> ch) : ch_(std::move(ch)), faultAt_(fault_abort_at()) {}
 
-  void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
-                 const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
-    SPFFT_TIMED_SCOPE("rccl_alltoallv");
+  void exchange(const void* send, void* recv, const std::vector<Transfer>& ts, hipStream_t stream,
+                const ExchangeSync* sync) override {
+    SPFFT_TIMED_SCOPE("rccl_exchange");
     if (++calls_ == faultAt_) ch_->abort();
     ch_->check_usable();
-    const int me = ch_->rank, P = ch_->size;
     const char* s = static_cast<const char*>(send);
     char* r = static_cast<char*>(recv);
-    // the local block never leaves the GPU
-    if (sc[me] > 0)
-      gpu_check(hipMemcpyAsync(r + rd[me], s + sd[me], static_cast<std::size_t>(sc[me]),
-                               hipMemcpyDeviceToDevice, stream),
-                "hipMemcpyAsync");
-    std::vector<NcclChannel::Xfer> xs;
-    xs.reserve(2 * P);
-    for (int k = 1; k < P; ++k) {
-      // staggered peer order so every xGMI link is busy from the start
-      const int to = (me + k) % P;
-      const int from = (me - k + P) % P;
-      if (sc[to] > 0) xs.push_back({s + sd[to], nullptr, static_cast<std::size_t>(sc[to]), to});
-      if (rc[from] > 0) xs.push_back({nullptr, r + rd[from], static_cast<std::size_t>(rc[from]), from});
+    std::vector<NcclChannel::Xfer> xs, local;
+    xs.reserve(ts.size());
+    for (const Transfer& t : ts) {
+      const std::size_t n = static_cast<std::size_t>(t.bytes);
+      switch (t.kind) {
+        case Transfer::kLocal:
+          local.push_back({s + t.offset, r + t.dstOffset, n, t.peer});
+          break;
+        case Transfer::kSend:
+          xs.push_back({s + t.offset, nullptr, n, t.peer});
+          break;
+        default:
+          xs.push_back({nullptr, r + t.offset, n, t.peer});
+      }
     }
-    if (!xs.empty()) ch_->run(xs, stream);
+    if (xs.empty() && local.empty() && !sync) return;
+    ch_->run(xs, local, stream, sync);
   }
+  int plane_rank() const override { return ch_->rank; }
+  int plane_size() const override { return ch_->size; }
   bool host_synchronous() const override { return false; }
+  hipStream_t channel_stream() const override { return ch_->stream->get(); }
   const char* kind() const override { return "rccl"; }
   bool healthy(std::string* detail) override { return ch_->healthy(detail); }
   void check() override {
@@ -249,46 +312,107 @@ private:
   int faultAt_ = 0, calls_ = 0;
 };
 
+// ExchangeSync on the caller's stream (host-synchronous planes)
+void sync_begin(const ExchangeSync* sync, hipStream_t stream) {
+  if (!sync) return;
+  if (sync->ready) gpu_check(hipStreamWaitEvent(stream, sync->ready, 0), "hipStreamWaitEvent");
+  if (sync->begin) gpu_check(hipEventRecord(sync->begin, stream), "hipEventRecord");
+}
+void sync_end(const ExchangeSync* sync, hipStream_t stream) {
+  if (!sync) return;
+  if (sync->done) gpu_check(hipEventRecord(sync->done, stream), "hipEventRecord");
+  if (sync->end) gpu_check(hipEventRecord(sync->end, stream), "hipEventRecord");
+}
+
+// In-process planes see every virtual rank's transfer list: the blocks rank
+// `me` receives are paired with the senders' lists by NCCL's matching rule (the
+// m-th send q -> me with the m-th receive me <- q; the own block with itself),
+// which is exactly what a multi-rank RCCL communicator does with the lists
+// RcclDeviceComm passes it.
+struct PlaneView {
+  const char* send;
+  const std::vector<Transfer>* xs;
+};
+struct Pairing {
+  const char* src;
+  char* dst;
+  std::size_t bytes;
+};
+bool pair_transfers(int me, const std::vector<PlaneView>& all, char* recv, std::vector<Pairing>& out) {
+  const int P = static_cast<int>(all.size());
+  const std::vector<Transfer>& mine = *all[me].xs;
+  for (int k = 0; k < P; ++k) {
+    const int q = (me - k + P) % P;
+    std::vector<const Transfer*> sends, recvs;
+    for (const Transfer& t : *all[q].xs)
+      if (q == me ? t.kind == Transfer::kLocal : (t.kind == Transfer::kSend && t.peer == me))
+        sends.push_back(&t);
+    for (const Transfer& t : mine)
+      if (q == me ? t.kind == Transfer::kLocal : (t.kind == Transfer::kRecv && t.peer == q))
+        recvs.push_back(&t);
+    if (sends.size() != recvs.size()) return false;
+    for (std::size_t m = 0; m < sends.size(); ++m) {
+      if (sends[m]->bytes != recvs[m]->bytes) return false;
+      const std::int64_t dst = q == me ? recvs[m]->dstOffset : recvs[m]->offset;
+      out.push_back({all[q].send + sends[m]->offset, recv + dst, static_cast<std::size_t>(sends[m]->bytes)});
+    }
+  }
+  return true;
+}
+
+// Collective: every virtual rank's list is visible, the receive side is
+// paired. All ranks fail together (an error flag is agreed before anyone
+// throws), so no virtual rank is left waiting in a later collective.
+std::vector<Pairing> pair_in_group(Communicator& comm, const void* send, void* recv,
+                                   const std::vector<Transfer>& xs) {
+  const int P = comm.size(), me = comm.rank();
+  PlaneView mine{static_cast<const char*>(send), &xs};
+  std::vector<PlaneView> all(P);
+  comm.allgather(&mine, all.data(), sizeof(PlaneView));
+  std::vector<Pairing> pairs;
+  int ok = pair_transfers(me, all, static_cast<char*>(recv), pairs) ? 1 : 0;
+  std::vector<int> oks(P);
+  comm.allgather(&ok, oks.data(), sizeof(int));
+  for (int v : oks)
+    if (!v) {
+      set_error_detail("exchange: transfer lists of the ranks do not match");
+      throw MPIError();
+    }
+  return pairs;
+}
+
 // In-process virtual ranks (local group) with every block moved by RCCL: each
 // virtual rank owns a size-1 RCCL communicator and receives the blocks of every
 // rank q (itself included) by a grouped ncclSend/ncclRecv pair to itself, on
-// the channel stream, with the real counts and displacements. This runs the
-// RCCL data path (group semantics, stream hand-off, byte layouts, async-error
-// polling, abort) on a single GPU, where RCCL refuses two ranks per device.
+// the channel stream, with the real transfer lists. This runs the RCCL data
+// path (group semantics, stream hand-off, byte layouts, async-error polling,
+// abort) on a single GPU inside one process.
 class RcclSelfDeviceComm : public DeviceComm {
 public:
   RcclSelfDeviceComm(const std::shared_ptr<Communicator>& comm, std::shared_ptr<NcclChannel> ch)
       : comm_(comm), ch_(std::move(ch)), faultAt_(fault_abort_at()) {}
 
-  void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
-                 const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
-    SPFFT_TIMED_SCOPE("rccl_self_alltoallv");
+  void exchange(const void* send, void* recv, const std::vector<Transfer>& xs, hipStream_t stream,
+                const ExchangeSync* sync) override {
+    SPFFT_TIMED_SCOPE("rccl_self_exchange");
     if (++calls_ == faultAt_) ch_->abort();
     ch_->check_usable();
-    const int P = comm_->size(), me = comm_->rank();
+    sync_begin(sync, stream);
     // every virtual rank's send buffer is complete before anyone pulls from it
     gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-    struct View {
-      const char* send;
-      const std::int64_t* counts;
-      const std::int64_t* displs;
-    };
-    View mine{static_cast<const char*>(send), sc, sd};
-    std::vector<View> all(P);
-    comm_->allgather(&mine, all.data(), sizeof(View));
-    std::vector<NcclChannel::Xfer> xs;
-    for (int k = 0; k < P; ++k) {
-      const int q = (me - k + P) % P;
-      const std::int64_t n = all[q].counts[me];
-      if (n != rc[q]) throw MPIError();
-      if (n <= 0) continue;
-      xs.push_back({all[q].send + all[q].displs[me], nullptr, static_cast<std::size_t>(n), 0});
-      xs.push_back({nullptr, static_cast<char*>(recv) + rd[q], static_cast<std::size_t>(n), 0});
+    const std::vector<Pairing> pairs = pair_in_group(*comm_, send, recv, xs);
+    std::vector<NcclChannel::Xfer> cx;
+    for (const Pairing& p : pairs) {
+      cx.push_back({p.src, nullptr, p.bytes, 0});
+      cx.push_back({nullptr, p.dst, p.bytes, 0});
     }
-    if (!xs.empty()) ch_->run(xs, stream);
+    if (!cx.empty()) ch_->run(cx, {}, stream, nullptr);
     gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     comm_->barrier();  // senders may reuse their buffers only after every pull
+    sync_end(sync, stream);
   }
+  int plane_rank() const override { return comm_->rank(); }
+  int plane_size() const override { return comm_->size(); }
   bool host_synchronous() const override { return true; }
   const char* kind() const override { return "rccl-self"; }
   bool healthy(std::string* detail) override { return ch_->healthy(detail); }
@@ -311,30 +435,19 @@ class LoopbackDeviceComm : public DeviceComm {
 public:
   explicit LoopbackDeviceComm(const std::shared_ptr<Communicator>& comm) : comm_(comm) {}
 
-  void alltoallv(const void* send, const std::int64_t* sc, const std::int64_t* sd, void* recv,
-                 const std::int64_t* rc, const std::int64_t* rd, hipStream_t stream) override {
-    SPFFT_TIMED_SCOPE("loopback_alltoallv");
-    const int P = comm_->size(), me = comm_->rank();
+  void exchange(const void* send, void* recv, const std::vector<Transfer>& xs, hipStream_t stream,
+                const ExchangeSync* sync) override {
+    SPFFT_TIMED_SCOPE("loopback_exchange");
+    sync_begin(sync, stream);
     gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-    struct View {
-      const char* send;
-      const std::int64_t* counts;
-      const std::int64_t* displs;
-    };
-    View mine{static_cast<const char*>(send), sc, sd};
-    std::vector<View> all(P);
-    comm_->allgather(&mine, all.data(), sizeof(View));
-    for (int q = 0; q < P; ++q) {
-      const std::int64_t n = all[q].counts[me];
-      if (n != rc[q]) throw MPIError();
-      if (n > 0)
-        gpu_check(hipMemcpyAsync(static_cast<char*>(recv) + rd[q], all[q].send + all[q].displs[me],
-                                 static_cast<std::size_t>(n), hipMemcpyDefault, stream),
-                  "hipMemcpyAsync");
-    }
+    for (const Pairing& p : pair_in_group(*comm_, send, recv, xs))
+      gpu_check(hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyDefault, stream), "hipMemcpyAsync");
     gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     comm_->barrier();  // senders may reuse their buffers only after every pull
+    sync_end(sync, stream);
   }
+  int plane_rank() const override { return comm_->rank(); }
+  int plane_size() const override { return comm_->size(); }
   bool host_synchronous() const override { return true; }
   const char* kind() const override { return "loopback"; }
 
@@ -435,10 +548,12 @@ public:
     if (failHost_) (void)hipHostFree(failHost_);
   }
 
-  void alltoallv(const void*, const std::int64_t*, const std::int64_t*, void*, const std::int64_t*,
-                 const std::int64_t*, hipStream_t) override {
+  void exchange(const void*, void*, const std::vector<Transfer>&, hipStream_t,
+                const ExchangeSync*) override {
     throw InternalError();  // the stage kernels move the data themselves
   }
+  int plane_rank() const override { return me_; }
+  int plane_size() const override { return P_; }
   bool host_synchronous() const override { return false; }
   bool peer_writes() const override { return true; }
   void* peer_buffer(int rank, int slot) const override { return peers_.at(rank).at(slot); }
@@ -508,6 +623,7 @@ struct NodeInfo {
   std::uint64_t host;
   long long pid;
   int domain, bus, device, ordinal;
+  unsigned long long channelDomain;  // Communicator::channel_domain
   int prefer;  // SPFFT_GPU_EXCHANGE: 0 auto, 1 rccl, 2 peer (ipc)
   int fault;   // SPFFT_FAULT_RCCL_INIT (rank 0's value is used everywhere)
 };
@@ -598,6 +714,20 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     if (unbuffered) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, false));
     return std::unique_ptr<DeviceComm>(new LoopbackDeviceComm(comm));
   }
+  // SPFFT_RCCL_VIRTUAL_HOSTS=1 (rehearsals on a box with fewer GPUs than
+  // ranks): RCCL refuses two ranks of one host on one device ("Duplicate
+  // GPU"), so every rank claims a host of its own (NCCL_HOSTID) and the ranks
+  // talk over RCCL's socket transport on loopback. The exchanges then run the
+  // multi-rank RcclDeviceComm path that ships to 8 GPUs: peer ids, staggered
+  // send/receive order, grouped calls, channel stream hand-offs.
+  const char* vh = std::getenv("SPFFT_RCCL_VIRTUAL_HOSTS");
+  const bool virtualHosts = vh && *vh == '1';
+  if (virtualHosts) {
+    const std::string id = "spfft-virtual-host-" + std::to_string(comm->rank());
+    setenv("NCCL_HOSTID", id.c_str(), 1);
+    setenv("NCCL_IB_DISABLE", "1", 0);
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+  }
   // data-plane choice, identical on every rank (decided from allgathered facts)
   NodeInfo mine{};
   mine.host = host_hash();
@@ -609,7 +739,8 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     (void)hipDeviceGetAttribute(&mine.bus, hipDeviceAttributePciBusId, device);
     (void)hipDeviceGetAttribute(&mine.device, hipDeviceAttributePciDeviceId, device);
   }
-  mine.prefer = prefLocal;
+  mine.channelDomain = comm->channel_domain();
+  mine.prefer = virtualHosts ? 1 : prefLocal;
   mine.fault = env_fault();
   const int P = comm->size();
   std::vector<NodeInfo> all(P);
@@ -621,9 +752,9 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     for (int r = 0; r < q; ++r)
       sharedDevice = sharedDevice || (all[q].host == all[r].host && all[q].domain == all[r].domain &&
                                       all[q].bus == all[r].bus && all[q].device == all[r].device);
-    char m[96];
-    std::snprintf(m, sizeof(m), "/%llx:%lld:%d.%d.%d", static_cast<unsigned long long>(all[q].host),
-                  all[q].pid, all[q].domain, all[q].bus, all[q].ordinal);
+    char m[128];
+    std::snprintf(m, sizeof(m), "/%llx:%lld:%d.%d.%d:%llx", static_cast<unsigned long long>(all[q].host),
+                  all[q].pid, all[q].domain, all[q].bus, all[q].ordinal, all[q].channelDomain);
     key += m;
   }
   // every rank decides from rank 0's settings (environments may differ)

@@ -26,16 +26,54 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "spfft/communicator.hpp"
 #include "spfft/types.h"
 
 namespace spfft {
 
-// Seconds a distributed call may wait for its data plane (RCCL initialisation,
-// the watched stream wait) before it aborts the data plane and throws
-// MPIError. SPFFT_COMM_TIMEOUT, default 120; 0 = no limit.
+// Seconds a distributed call may wait for its exchange (the watched stream
+// wait) before it aborts the data plane and throws MPIError.
+// SPFFT_COMM_TIMEOUT, default 0 = no limit (MPI semantics: a slow peer is not
+// an error).
 double comm_timeout_seconds();
+// Deadline of the collective RCCL initialisation: SPFFT_COMM_TIMEOUT when set
+// and > 0, else 300 s (a rank that never arrives must not leave the others
+// inside RCCL forever).
+double comm_init_timeout_seconds();
+
+// One point-to-point transfer of an exchange as issued to the data plane.
+struct Transfer {
+  enum Kind : int { kSend = 0, kRecv = 1, kLocal = 2 };
+  int kind;
+  int peer;                // destination (kSend), source (kRecv); the own rank for kLocal
+  std::int64_t offset;     // bytes into the send buffer (kSend, kLocal source) or receive buffer (kRecv)
+  std::int64_t dstOffset;  // kLocal: bytes into the receive buffer
+  std::int64_t bytes;
+};
+
+// Appends the transfer list of one all-to-all-v (byte counts and
+// displacements, one entry per rank) to `out`: the own block first (kLocal),
+// then the peers in staggered order, k = 1..P-1: send to me+k, receive from
+// me-k, so that every xGMI link carries traffic from the start. Zero-byte
+// blocks are omitted. Every data plane pairs the m-th send q -> r with the m-th
+// receive r <- q (NCCL's point-to-point matching rule).
+void append_alltoallv(std::vector<Transfer>& out, int me, int P, const std::int64_t* sendCounts,
+                      const std::int64_t* sendDispls, const std::int64_t* recvCounts,
+                      const std::int64_t* recvDispls);
+
+// Stream hand-off of an asynchronous exchange (pipelined plans): the transfers
+// start after `ready` (recorded by the caller; null = no wait) and `done` is
+// recorded once every block has arrived. The caller's stream does not wait.
+// `begin` / `end` (optional timing events) are recorded right before the
+// transfers start and after they completed, on the stream that runs them.
+struct ExchangeSync {
+  hipEvent_t ready;
+  hipEvent_t done;
+  hipEvent_t begin;
+  hipEvent_t end;
+};
 
 class DeviceComm {
 public:
@@ -45,14 +83,24 @@ public:
                                             SpfftExchangeType exchange, void* const buffers[2]);
   virtual ~DeviceComm();
 
-  // Byte counts / displacements, one entry per rank. Enqueued on `stream`;
-  // the receive buffer is complete when the stream reaches this point.
-  virtual void alltoallv(const void* send, const std::int64_t* sendCounts,
-                         const std::int64_t* sendDispls, void* recv,
-                         const std::int64_t* recvCounts, const std::int64_t* recvDispls,
-                         hipStream_t stream) = 0;
-  // true if alltoallv() returns only after the data moved (host-synchronous).
+  // Runs a transfer list (collective: every rank calls with its own list).
+  // sync == nullptr: enqueued after the work on `stream`, and `stream` waits
+  // until every block has arrived. Otherwise see ExchangeSync; data planes
+  // without a stream of their own run it on `stream`.
+  virtual void exchange(const void* send, void* recv, const std::vector<Transfer>& xs,
+                        hipStream_t stream, const ExchangeSync* sync) = 0;
+  // Byte counts / displacements, one entry per rank, as one exchange().
+  void alltoallv(const void* send, const std::int64_t* sendCounts, const std::int64_t* sendDispls,
+                 void* recv, const std::int64_t* recvCounts, const std::int64_t* recvDispls,
+                 hipStream_t stream);
+  // This rank and the number of ranks of the exchange (entries of alltoallv's arrays).
+  virtual int plane_rank() const = 0;
+  virtual int plane_size() const = 0;
+  // true if exchange() returns only after the data moved (host-synchronous).
   virtual bool host_synchronous() const = 0;
+  // The stream that carries this plane's asynchronous exchanges (the RCCL
+  // channel stream shared by every grid of the process), null if none.
+  virtual hipStream_t channel_stream() const { return nullptr; }
 
   // Peer-write data plane: stage kernels store into peer_buffer(r, slot)
   // directly. Every rank issues the same sequence of calls (transforms are

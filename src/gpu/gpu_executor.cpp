@@ -63,8 +63,9 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   }
   setup_long_axes();
 
-  ownStream_.reset(new GpuStream());
-  stream_ = ownStream_->get();
+  // the private stream is created on first use: a transform that runs on a
+  // user stream (set_stream before its first call) never owns one
+  stream_ = nullptr;
   event_.reset(new GpuEvent());
 
   // device tables (uploaded once; the hot path never touches the host plan)
@@ -120,30 +121,39 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
       upload_ztab(zTab_, sdl);
       bwdSendCounts_[p.rank] = bwdRecvCounts_[p.rank] = 0;
     }
-    // Exchange pipelining over plane chunks (build_chunk_plan): chunk k's
-    // all-to-all overlaps the y/x stages of chunk k-1 (backward) or k+1
-    // (forward). Model: a chunk pays one grouped send/recv launch (~10-20 us
-    // of fixed cost) and per-peer messages below ~1.5 MB lose link efficiency,
-    // so K = per-peer bytes / 1.5 MB, between 1 and 4. 256^3 C2C fp64 sends
-    // 3.3 MB per peer at P = 8 (K = 2), 13 MB at P = 4 and 53 MB at P = 2
-    // (K = 4). Computed from global quantities so every rank agrees;
-    // SPFFT_EXCH_CHUNKS forces a count (rank 0's value is used everywhere).
-    // The peer-write plane needs none: its stores are issued by the stage
-    // kernels themselves and overlap their compute wave by wave.
+    // Exchange pipelining (build_chunk_plan): K plane chunks, so chunk k's
+    // exchange overlaps the y/x stages of chunk k-1 (backward) or k+1
+    // (forward), and I stick blocks, so block i's exchange overlaps the z stage
+    // of block i+1 (backward) or i-1 (forward). Model: a step pays one grouped
+    // send/recv launch (~10-20 us of fixed cost) and per-peer messages below
+    // ~1.5 MB lose link efficiency, so K = per-peer bytes / 1.5 MB, between 1
+    // and 4. 256^3 C2C fp64 sends 3.3 MB per peer at P = 8 (K = 2), 13 MB at
+    // P = 4 and 53 MB at P = 2 (K = 4). The z stage is about a third of the
+    // compute; splitting it pays only when the exchange dwarfs the step
+    // overhead: I = 2 from 8 MB per peer (256^3 fp64 at P <= 4), else 1.
+    // Computed from global quantities so every rank agrees;
+    // SPFFT_EXCH_CHUNKS / SPFFT_EXCH_STICK_BLOCKS force the counts (rank 0's
+    // values are used everywhere). The peer-write plane needs none: its stores
+    // are issued by the stage kernels themselves and overlap their compute wave
+    // by wave.
     const double perPeer = static_cast<double>(p.totalSticks) * p.dimZ * eb /
                            (static_cast<double>(p.size) * p.size);
     chunkModel_ = perPeer;
     int chunks = static_cast<int>(std::min(4.0, std::max(1.0, std::floor(perPeer / (1.5 * (1 << 20))))));
     chunks = env_int("SPFFT_EXCH_CHUNKS", chunks, 1, 64);
-    if (peerWrites_) chunks = 1;
-    // rank 0's count, reduced until the (padded) layout fits every rank's buffers
-    int req[2] = {chunks, 1};
+    int blocks = perPeer >= 8.0 * (1 << 20) ? 2 : 1;
+    blocks = env_int("SPFFT_EXCH_STICK_BLOCKS", blocks, 1, 16);
+    if (peerWrites_) chunks = blocks = 1;
+    // rank 0's counts; the chunk count reduced until the (padded) layout fits
+    // every rank's buffers
+    int req[3] = {chunks, 1, blocks};
     while (req[1] < chunks && chunk_plan_fits(req[1] + 1)) ++req[1];
-    std::vector<int> all(2 * p.size);
+    std::vector<int> all(3 * p.size);
     grid_->communicator()->allgather(req, all.data(), sizeof(req));
     chunks = all[0];
-    for (int r = 0; r < p.size; ++r) chunks = std::min(chunks, all[2 * r + 1]);
-    if (chunks > 1 && !build_chunk_plan(chunks)) throw InternalError();
+    blocks = all[2];
+    for (int r = 0; r < p.size; ++r) chunks = std::min(chunks, all[3 * r + 1]);
+    if (chunks * blocks > 1 && !build_chunk_plan(chunks, blocks)) throw InternalError();
   }
   log_plan();
 }
@@ -165,16 +175,18 @@ void GpuExecutor<T>::log_plan() const {
   if (p.size > 1) plane = const_cast<GridImpl<T>&>(*grid_).device_comm().describe();
   std::fprintf(stderr,
                "spfft[gpu rank %d/%d] %dx%dx%d %s %s: sticks=%d planes=%d columns=%d | z{%s} "
-               "y{%s} x{%s}%s inter_planes=%d | exchange=%s%s plane=%s chunks=%d (%.2f MB per "
-               "peer) peer_writes=%d peer_offsets=[%lld, %lld]\n",
+               "y{%s} x{%s}%s inter_planes=%d | exchange=%s%s plane=%s chunks=%d stick_blocks=%d "
+               "steps=%zu+%zu (%.2f MB per peer) peer_writes=%d peer_offsets=[%lld, %lld] "
+               "library_streams=%d\n",
                p.rank, p.size, p.dimX, p.dimY, p.dimZ,
                p.type == SPFFT_TRANS_R2C ? "R2C" : "C2C", dbl ? "fp64" : "fp32", p.local_sticks(),
                p.local_planes(), p.num_columns(),
                describe(longZ_, lpZ_, p.dimZ, false).c_str(), describe(longY_, lpY_, p.dimY, true).c_str(),
                describe(longX_, lpX_, twXh_ ? p.dimX / 2 : p.dimX, true).c_str(),
                twXh_ ? " packed-real" : "", interPlanes_, layout_.buffered ? "buffered" : "compact",
-               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, chunkModel_ / 1e6,
-               peerWrites_ ? 1 : 0, peerOffsetRange_[0], peerOffsetRange_[1]);
+               floatExchange_ ? "-float" : "", plane.c_str(), exchChunks_, stickBlocks_, bwdSteps_.size(),
+               fwdSteps_.size(), chunkModel_ / 1e6, peerWrites_ ? 1 : 0, peerOffsetRange_[0],
+               peerOffsetRange_[1], GpuStream::live());
 }
 
 template <typename T>
@@ -233,12 +245,12 @@ bool GpuExecutor<T>::chunk_plan_fits(int K) const {
 }
 
 template <typename T>
-bool GpuExecutor<T>::build_chunk_plan(int K) {
+bool GpuExecutor<T>::build_chunk_plan(int K, int I) {
   const IndexPlan& p = *plan_;
   const int P = p.size, me = p.rank;
-  // K depends on global quantities only: every rank issues the same number of
-  // all-to-all rounds (a rank with fewer planes than K gets empty chunks)
-  if (K < 2) return false;
+  // K and I depend on global quantities only: every rank issues the same
+  // exchange steps (a rank with fewer planes or sticks gets empty ones)
+  if (K < 1 || I < 1 || K * I < 2) return false;
   const bool buf = layout_.buffered;
   const i64 eb = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   auto pb = [&](int r, int k) -> i64 { return static_cast<i64>(p.planesPerRank[r]) * k / K; };
@@ -246,6 +258,9 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
   const i64 Mk = (static_cast<i64>(p.maxPlanes) + K - 1) / K;  // padded chunk (BUFFERED)
   const i64 rowsPad = p.maxSticks;
   auto stride = [&](int r, int k) -> i64 { return buf ? Mk : pb(r, k + 1) - pb(r, k); };
+  // rows of rank q's sticks on the wire, and the first row of its block i
+  auto rows = [&](int q) -> i64 { return buf ? rowsPad : static_cast<i64>(p.sticksPerRank[q]); };
+  auto rb = [&](int q, int i) -> i64 { return rows(q) * i / I; };
   const int NV = K * P;
   std::vector<long long> segDispl(NV), segStride(NV);
   std::vector<int> segZOff(NV), zSeg(p.dimZ, 0);
@@ -258,7 +273,7 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
       segStride[v] = stride(r, k);
       segZOff[v] = p.planeOffsets[r] + static_cast<int>(pb(r, k));
       for (i64 z = 0; z < n; ++z) zSeg[segZOff[v] + z] = v;
-      off += (buf ? rowsPad : S) * segStride[v];
+      off += rows(me) * segStride[v];
     }
   }
   if (off > grid_->slot_elements(GridImpl<T>::kStickSide)) return false;
@@ -267,16 +282,18 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
   for (int k = 0; k < K; ++k) {
     for (int q = 0; q < P; ++q) {
       slabDispl[k * P + q] = soff;
-      soff += (buf ? rowsPad : static_cast<i64>(p.sticksPerRank[q])) * stride(me, k);
+      soff += rows(q) * stride(me, k);
     }
   }
   if (soff > grid_->slot_elements(GridImpl<T>::kSlabSide)) return false;
   if (!buf && (off != layout_.stickTotal || soff != layout_.slabTotal)) throw InternalError();
   planeBounds_.resize(K + 1);
   for (int k = 0; k <= K; ++k) planeBounds_[k] = static_cast<int>(pb(me, k));
+  // z launch i covers the sticks of message rows [rb(me, i), rb(me, i + 1))
+  stickBounds_.resize(I + 1);
+  for (int i = 0; i <= I; ++i) stickBounds_[i] = static_cast<int>(std::min(S, rb(me, i)));
   colBaseChunk_.clear();
   colDescChunk_.clear();
-  chunks_.assign(K, ChunkXfer{});
   for (int k = 0; k < K; ++k) {
     const i64 sk = stride(me, k);
     // entry e at local plane z of chunk k: base + z (z in [pb_k, pb_k+1))
@@ -287,30 +304,75 @@ bool GpuExecutor<T>::build_chunk_plan(int K) {
     upload(colBaseChunk_.back(), cb);
     colDescChunk_.emplace_back();
     build_col_desc(colDescChunk_.back(), cb, sk);
-    ChunkXfer& c = chunks_[k];
+  }
+  // transfer list of message (i, k) in the backward direction
+  auto cell = [&](int i, int k, std::vector<Transfer>& out) {
+    std::vector<std::int64_t> sc(P), sd(P), rc(P), rd(P);
     for (int r = 0; r < P; ++r) {
       const int v = k * P + r;
-      c.sd.push_back(segDispl[v] * eb);
-      c.sc.push_back((buf ? rowsPad : S) * segStride[v] * eb);
-      c.rd.push_back(slabDispl[v] * eb);
-      c.rc.push_back((buf ? rowsPad : static_cast<i64>(p.sticksPerRank[r])) * sk * eb);
+      sd[r] = (segDispl[v] + rb(me, i) * segStride[v]) * eb;
+      sc[r] = (rb(me, i + 1) - rb(me, i)) * segStride[v] * eb;
+      rd[r] = (slabDispl[v] + rb(r, i) * stride(me, k)) * eb;
+      rc[r] = (rb(r, i + 1) - rb(r, i)) * stride(me, k) * eb;
     }
-    if (localDirect_) {
-      // own block in place on the slab side (see the constructor)
-      segDispl[k * P + me] = slab_offset() + slabDispl[k * P + me];
-      c.sc[me] = c.rc[me] = 0;
-    }
+    if (localDirect_) sc[me] = rc[me] = 0;  // own block in place on the slab side
+    append_alltoallv(out, me, P, sc.data(), sd.data(), rc.data(), rd.data());
+  };
+  // backward: blocks 0..I-2 as soon as their z launch is done, each with every
+  // chunk; the last block chunk by chunk, chunk k's arrival releases y/x(k)
+  bwdSteps_.clear();
+  for (int i = 0; i + 1 < I; ++i) {
+    ExchangeStep st{{}, 1, i, 0, 0};
+    for (int k = 0; k < K; ++k) cell(i, k, st.xs);
+    bwdSteps_.push_back(std::move(st));
   }
+  for (int k = 0; k < K; ++k) {
+    ExchangeStep st{{}, k == 0 ? 1 : 0, I - 1, 2, k};
+    cell(I - 1, k, st.xs);
+    bwdSteps_.push_back(std::move(st));
+  }
+  // forward (send and receive roles swapped): chunks 0..K-2 as soon as their y
+  // stage is done, each with every block; the last chunk block by block, block
+  // i's arrival releases z(i)
+  auto mirror = [](std::vector<Transfer>& xs) {
+    for (Transfer& t : xs) {
+      if (t.kind == Transfer::kLocal)
+        std::swap(t.offset, t.dstOffset);
+      else
+        t.kind = t.kind == Transfer::kSend ? Transfer::kRecv : Transfer::kSend;
+    }
+    // a receive from q mirrors into a send to q: the staggered order of the
+    // backward list (send me+k, receive me-k) becomes (receive me+k, send
+    // me-k), which pairs across ranks in the same order
+  };
+  fwdSteps_.clear();
+  for (int k = 0; k + 1 < K; ++k) {
+    ExchangeStep st{{}, 2, k, 0, 0};
+    for (int i = 0; i < I; ++i) cell(i, k, st.xs);
+    mirror(st.xs);
+    fwdSteps_.push_back(std::move(st));
+  }
+  for (int i = 0; i < I; ++i) {
+    ExchangeStep st{{}, i == 0 ? 2 : 0, K - 1, 3, i};
+    cell(i, K - 1, st.xs);
+    mirror(st.xs);
+    fwdSteps_.push_back(std::move(st));
+  }
+  if (localDirect_)
+    for (int k = 0; k < K; ++k) segDispl[k * P + me] = slab_offset() + slabDispl[k * P + me];
   zSeg_ = zSeg;
   segStride_ = segStride;
   segZOff_ = segZOff;
   upload_ztab(zTab_, segDispl);
   exchChunks_ = K;
-  commStream_.reset(new GpuStream(true));
-  chunkEvents_.clear();
-  for (int k = 0; k < K; ++k) chunkEvents_.emplace_back(new GpuEvent());
-  commDone_.reset(new GpuEvent());
-  zDone_.reset(new GpuEvent());
+  stickBlocks_ = I;
+  auto events = [](std::vector<std::unique_ptr<GpuEvent>>& v, int n) {
+    v.clear();
+    for (int j = 0; j < n; ++j) v.emplace_back(new GpuEvent());
+  };
+  events(zEv_, I);
+  events(blockEv_, I);
+  events(chunkEv_, K);
   return true;
 }
 
@@ -342,32 +404,51 @@ long long GpuExecutor<T>::slab_offset() const {
 }
 
 template <typename T>
-void GpuExecutor<T>::pipelined_exchange(bool backward) {
+hipEvent_t GpuExecutor<T>::step_event(int kind, int idx) const {
+  switch (kind) {
+    case 1:
+      return zEv_[idx]->get();
+    case 2:
+      return chunkEv_[idx]->get();
+    case 3:
+      return blockEv_[idx]->get();
+    default:
+      return nullptr;
+  }
+}
+
+template <typename T>
+void GpuExecutor<T>::run_steps(const std::vector<ExchangeStep>& steps, bool backward) {
   DeviceGuard guard(deviceId_);
   void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   DeviceComm& dc = grid_->device_comm();
-  hipStream_t cs = commStream_->get();
-  if (backward) {
-    // the whole z stage precedes every chunk; the y/x stages of chunk k wait on
-    // chunkEvents_[k] (backward_xy)
-    zDone_->record(stream_);
-    zDone_->wait_on(cs);
-    for (int k = 0; k < exchChunks_; ++k) {
-      const ChunkXfer& c = chunks_[k];
-      dc.alltoallv(stick, c.sc.data(), c.sd.data(), slab, c.rc.data(), c.rd.data(), cs);
-      chunkEvents_[k]->record(cs);
-    }
-    return;
+  // SPFFT_TIMING: the span from the first step's start to the last step's
+  // completion on the data plane's stream (gpu/<direction>/exchange-span)
+  GpuEvent *b = nullptr, *e = nullptr;
+  if (timing::enabled() && !capturing_ && !steps.empty()) {
+    spans_.push_back(ExchangeSpan{backward ? "backward" : "forward", timing_event(), timing_event()});
+    b = spans_.back().begin.get();
+    e = spans_.back().end.get();
   }
-  // chunk k's y stage recorded chunkEvents_[k] (forward_xy)
-  for (int k = 0; k < exchChunks_; ++k) {
-    chunkEvents_[k]->wait_on(cs);
-    const ChunkXfer& c = chunks_[k];
-    dc.alltoallv(slab, c.rc.data(), c.rd.data(), stick, c.sc.data(), c.sd.data(), cs);
+  for (std::size_t j = 0; j < steps.size(); ++j) {
+    const ExchangeStep& st = steps[j];
+    const ExchangeSync sync{step_event(st.readyKind, st.readyIdx), step_event(st.doneKind, st.doneIdx),
+                            j == 0 && b ? b->get() : nullptr,
+                            j + 1 == steps.size() && e ? e->get() : nullptr};
+    if (backward)
+      dc.exchange(stick, slab, st.xs, stream_, &sync);
+    else
+      dc.exchange(slab, stick, st.xs, stream_, &sync);
   }
-  commDone_->record(cs);
-  commDone_->wait_on(stream_);
+}
+
+template <typename T>
+void GpuExecutor<T>::pipelined_exchange(bool backward) {
+  // backward: z(i) recorded zEv_[i] (backward_z); y/x(k) wait for chunkEv_[k]
+  // (backward_xy). forward: y(k) recorded chunkEv_[k] (forward_xy); z(i) waits
+  // for blockEv_[i] (forward_z)
+  run_steps(backward ? bwdSteps_ : fwdSteps_, backward);
 }
 
 template <typename T>
@@ -441,15 +522,24 @@ void GpuExecutor<T>::set_stream(hipStream_t stream, bool synchronous) {
 
 template <typename T>
 void GpuExecutor<T>::reset_stream() {
-  stream_ = ownStream_->get();
   ownStreamActive_ = true;
   synchronous_ = true;
+  stream_ = nullptr;
+  use_private_stream();
+}
+
+template <typename T>
+void GpuExecutor<T>::use_private_stream() {
+  if (!ownStreamActive_ || stream_) return;
+  DeviceGuard guard(deviceId_);
+  if (!ownStream_) ownStream_.reset(new GpuStream());
+  stream_ = ownStream_->get();
 }
 
 template <typename T>
 void GpuExecutor<T>::synchronize() {
   wait_stream();
-  if (!traces_.empty()) harvest_stage_times(false);
+  if (!traces_.empty() || !spans_.empty()) harvest_stage_times(false);
   // a peer barrier that timed out leaves a flag behind (data are incomplete)
   if (peerWrites_) grid_->device_comm().check();
 }
@@ -486,19 +576,39 @@ void GpuExecutor<T>::stage_mark(const char* dir, const char* stage) {
   }
   if (traces_.empty() || traces_.back().dir != dir) return;
   StageMark m;
-  if (!spareEvents_.empty()) {
-    m.ev = std::move(spareEvents_.back());
-    spareEvents_.pop_back();
-  } else {
-    m.ev.reset(new GpuEvent(true));
-  }
+  m.ev = timing_event();
   m.ev->record(stream_);
   m.stage = stage;
   traces_.back().marks.push_back(std::move(m));
 }
 
 template <typename T>
+std::unique_ptr<GpuEvent> GpuExecutor<T>::timing_event() {
+  if (spareEvents_.empty()) return std::unique_ptr<GpuEvent>(new GpuEvent(true));
+  std::unique_ptr<GpuEvent> ev = std::move(spareEvents_.back());
+  spareEvents_.pop_back();
+  return ev;
+}
+
+template <typename T>
 void GpuExecutor<T>::harvest_stage_times(bool wait) {
+  std::size_t spansDone = 0;
+  for (auto& sp : spans_) {
+    if (wait) {
+      gpu_check(hipEventSynchronize(sp.end->get()), "hipEventSynchronize");
+    } else {
+      const hipError_t e = hipEventQuery(sp.end->get());
+      if (e == hipErrorNotReady) break;
+      gpu_check(e, "hipEventQuery");
+    }
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, sp.begin->get(), sp.end->get()) == hipSuccess)
+      timing::add_sample({"gpu", sp.dir, "exchange-span"}, 1e-3 * ms);
+    spareEvents_.push_back(std::move(sp.begin));
+    spareEvents_.push_back(std::move(sp.end));
+    ++spansDone;
+  }
+  spans_.erase(spans_.begin(), spans_.begin() + static_cast<std::ptrdiff_t>(spansDone));
   std::size_t done = 0;
   for (auto& t : traces_) {
     if (t.marks.empty()) {
@@ -654,6 +764,7 @@ bool GpuExecutor<T>::forward_graph(SpfftProcessingUnitType inputLocation, T* out
 
 template <typename T>
 void GpuExecutor<T>::order_after_default_stream() {
+  use_private_stream();
   if (capturing_) return;
   // errors left behind by earlier (user) GPU work (reference: execution_gpu.cpp:251-253)
   if (hipGetLastError() != hipSuccess) throw GPUPrecedingError();
@@ -791,6 +902,21 @@ void GpuExecutor<T>::backward_z(const T* input) {
     a.zTab = zTabRemote_->data<long long>();
     a.remote = 1;
   }
+  // pipelined plans: one launch per stick block, whose messages leave as soon
+  // as it is done (zEv_, run_steps)
+  const int I = pipelined() ? stickBlocks_ : 1;
+  for (int i = 0; i < I; ++i) {
+    if (pipelined()) {
+      a.stickBegin = stickBounds_[i];
+      a.numSticks = stickBounds_[i + 1];
+    }
+    z_backward_launch(a, values, stick);
+    if (pipelined()) zEv_[i]->record(stream_);
+  }
+}
+
+template <typename T>
+void GpuExecutor<T>::z_backward_launch(const dev::ZArgs& a, const cx<T>* values, void* stick) {
   if (longZ_ && floatExchange_)
     dev::launch_long_z_backward<T, cx<float>>(lpZ_, a, values, static_cast<cx<float>*>(stick),
                                               long_bufs(), stream_);
@@ -824,13 +950,13 @@ template <typename T>
 void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_backward_exchange");
   // pipelined: the exchange runs on the comm stream, inside "exchange+y+x"
-  StageEnd stageEnd{this, "backward", exchChunks_ > 1 ? nullptr : "exchange"};
+  StageEnd stageEnd{this, "backward", pipelined() ? nullptr : "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
     return;
   }
-  if (exchChunks_ > 1) {
+  if (pipelined()) {
     pipelined_exchange(true);
     return;
   }
@@ -947,24 +1073,25 @@ void GpuExecutor<T>::backward_xy(SpfftProcessingUnitType outputLocation) {
   if (outputLocation != SPFFT_PU_HOST && outputLocation != SPFFT_PU_GPU)
     throw InvalidParameterError();
   DeviceGuard guard(deviceId_);
-  StageEnd stageEnd{this, "backward", exchChunks_ > 1 ? "exchange+y+x" : "y+x"};
+  StageEnd stageEnd{this, "backward", pipelined() ? "exchange+y+x" : "y+x"};
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   auto* inter = static_cast<cx<T>*>(grid_->device_slot(GridImpl<T>::kInter));
   void* space = grid_->device_slot(GridImpl<T>::kSpace);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kSlabSide);
   // pipelined exchange: the y/x stages of chunk k start when it has arrived;
   // within a chunk, plane ranges of at most interPlanes_ reuse the intermediate
-  const int K = exchChunks_ > 1 ? exchChunks_ : 1;
+  const bool pipe = pipelined();
+  const int K = pipe ? exchChunks_ : 1;
   for (int k = 0; k < K; ++k) {
-    if (K > 1) chunkEvents_[k]->wait_on(stream_);
-    const int zb = K > 1 ? planeBounds_[k] : 0;
-    const int ze = K > 1 ? planeBounds_[k + 1] : plan_->local_planes();
+    if (pipe) chunkEv_[k]->wait_on(stream_);
+    const int zb = pipe ? planeBounds_[k] : 0;
+    const int ze = pipe ? planeBounds_[k + 1] : plan_->local_planes();
     for (int z0 = zb; z0 < ze; z0 += interPlanes_) {
       auto ya = yargs();
       auto xa = xargs();
       ya.zBegin = xa.zBegin = z0;
       ya.L = xa.L = std::min(ze, z0 + interPlanes_);
-      if (K > 1) {
+      if (pipe) {
         ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
         set_col_desc(ya, colDescChunk_[k]);
       }
@@ -1003,16 +1130,17 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
   if (peerWrites_) grid_->device_comm().prepare_write(GridImpl<T>::kStickSide, stream_);
   // pipelined exchange: chunk k's all-to-all starts when its y stage is done;
   // within a chunk, plane ranges of at most interPlanes_ reuse the intermediate
-  const int K = exchChunks_ > 1 ? exchChunks_ : 1;
+  const bool pipe = pipelined();
+  const int K = pipe ? exchChunks_ : 1;
   for (int k = 0; k < K; ++k) {
-    const int zb = K > 1 ? planeBounds_[k] : 0;
-    const int ze = K > 1 ? planeBounds_[k + 1] : plan_->local_planes();
+    const int zb = pipe ? planeBounds_[k] : 0;
+    const int ze = pipe ? planeBounds_[k + 1] : plan_->local_planes();
     for (int z0 = zb; z0 < ze; z0 += interPlanes_) {
       auto ya = yargs();
       auto xa = xargs();
       ya.zBegin = xa.zBegin = z0;
       ya.L = xa.L = std::min(ze, z0 + interPlanes_);
-      if (K > 1) {
+      if (pipe) {
         ya.colBase = colBaseChunk_[k] ? colBaseChunk_[k]->data<long long>() : nullptr;
         set_col_desc(ya, colDescChunk_[k]);
       } else if (peerWrites_) {
@@ -1024,7 +1152,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       x_forward_launch(xa, space, out);
       y_forward_launch(ya, out, slab);
     }
-    if (K > 1) chunkEvents_[k]->record(stream_);
+    if (pipe) chunkEv_[k]->record(stream_);
   }
 }
 
@@ -1032,13 +1160,13 @@ template <typename T>
 void GpuExecutor<T>::forward_exchange(bool /*nonBlocking*/) {
   SPFFT_TIMED_SCOPE("gpu_forward_exchange");
   // pipelined: only the exchange's tail after the last y stage is left here
-  StageEnd stageEnd{this, "forward", exchChunks_ > 1 ? "exchange-tail" : "exchange"};
+  StageEnd stageEnd{this, "forward", pipelined() ? "exchange-tail" : "exchange"};
   if (peerWrites_) {
     DeviceGuard guard(deviceId_);
     grid_->device_comm().complete_writes(stream_);
     return;
   }
-  if (exchChunks_ > 1) {
+  if (pipelined()) {
     pipelined_exchange(false);
     return;
   }
@@ -1061,19 +1189,28 @@ void GpuExecutor<T>::forward_z(T* output, SpfftScalingType scaling) {
   if (hostOut) values = staging(p.numLocalElements);
   const void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   if (peerWrites_) grid_->device_comm().note_read(GridImpl<T>::kStickSide);
-  const auto a = zargs();
-  if (longZ_ && floatExchange_)
-    dev::launch_long_z_forward<T, cx<float>>(lpZ_, a, static_cast<const cx<float>*>(stick), values,
-                                             factor, long_bufs(), stream_);
-  else if (longZ_)
-    dev::launch_long_z_forward<T, cx<T>>(lpZ_, a, static_cast<const cx<T>*>(stick), values, factor,
-                                         long_bufs(), stream_);
-  else if (floatExchange_)
-    dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,
-                                        twZ_->data<cx<T>>(), stream_);
-  else
-    dev::launch_z_forward<T, cx<T>>(a, static_cast<const cx<T>*>(stick), values, factor,
-                                    twZ_->data<cx<T>>(), stream_);
+  auto a = zargs();
+  // pipelined plans: z(i) starts once stick block i has arrived
+  const int I = pipelined() ? stickBlocks_ : 1;
+  for (int i = 0; i < I; ++i) {
+    if (pipelined()) {
+      blockEv_[i]->wait_on(stream_);
+      a.stickBegin = stickBounds_[i];
+      a.numSticks = stickBounds_[i + 1];
+    }
+    if (longZ_ && floatExchange_)
+      dev::launch_long_z_forward<T, cx<float>>(lpZ_, a, static_cast<const cx<float>*>(stick), values,
+                                               factor, long_bufs(), stream_);
+    else if (longZ_)
+      dev::launch_long_z_forward<T, cx<T>>(lpZ_, a, static_cast<const cx<T>*>(stick), values, factor,
+                                           long_bufs(), stream_);
+    else if (floatExchange_)
+      dev::launch_z_forward<T, cx<float>>(a, static_cast<const cx<float>*>(stick), values, factor,
+                                          twZ_->data<cx<T>>(), stream_);
+    else
+      dev::launch_z_forward<T, cx<T>>(a, static_cast<const cx<T>*>(stick), values, factor,
+                                      twZ_->data<cx<T>>(), stream_);
+  }
   if (hostOut) {
     gpu_check(hipMemcpyAsync(output, values, sizeof(cx<T>) * p.numLocalElements,
                              hipMemcpyDeviceToHost, stream_),
@@ -1123,7 +1260,7 @@ void GpuExecutor<T>::compute_batch_key() {
 
 template <typename T>
 bool GpuExecutor<T>::batchable() const {
-  return batchEnabled_ && plan_->size == 1 && !peerWrites_ && exchChunks_ <= 1 && !capturing_ &&
+  return batchEnabled_ && plan_->size == 1 && !peerWrites_ && !pipelined() && !capturing_ &&
          !poison_ && interPlanes_ >= plan_->local_planes() && !longX_ && !longY_ && !longZ_;
 }
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "api/grid_impl.hpp"
+#include "gpu/device_comm.hpp"
 #include "gpu/gpu_runtime.hpp"
 #include "kernels/long_fft.hpp"
 #include "kernels/stage_args.hpp"
@@ -67,15 +68,20 @@ public:
   void set_stream(hipStream_t stream, bool synchronous);
   void reset_stream();
   hipStream_t stream() const { return stream_; }
+  // Creates the private stream now if the transform runs on it (it is
+  // otherwise created by the first call).
+  void ensure_stream() { use_private_stream(); }
   T* space_domain(SpfftProcessingUnitType location);
 
 private:
   template <typename U>
   U* upload(std::unique_ptr<DeviceBuffer>& buf, const std::vector<U>& v);
   void order_after_default_stream();
+  void use_private_stream();  // creates the private stream on first use
+  void z_backward_launch(const dev::ZArgs& a, const cx<T>* values, void* stick);
   void exchange(bool backward);
   void build_peer_tables();
-  bool build_chunk_plan(int chunks);
+  bool build_chunk_plan(int chunks, int blocks);
   bool chunk_plan_fits(int chunks) const;
   void pipelined_exchange(bool backward);
   void wait_stream();
@@ -177,25 +183,34 @@ private:
   std::unique_ptr<DeviceBuffer> colBaseRemote_;
   long long peerOffsetRange_[2] = {0, 0};  // min / max remote base (SPFFT_LOG)
 
-  // Pipelined exchange (RCCL / loopback data planes, compact layout): every
-  // rank's planes are split into K chunks and both exchange buffers are laid
-  // out chunk-major, so chunk k is one contiguous block per peer. Backward: the
-  // z stage runs whole, chunk k's all-to-all runs on commStream_ and the y/x
-  // stages of chunk k start as soon as it has arrived (while chunk k+1 is in
-  // flight). Forward: the x/y stages run per chunk and chunk k's all-to-all
-  // starts when its y stage is done. The exchange overlaps the y and x stages,
-  // two thirds of the compute, in both directions.
-  struct ChunkXfer {
-    std::vector<std::int64_t> sc, sd, rc, rd;  // bytes per rank (backward direction)
+  // Pipelined exchange (RCCL / loopback data planes): a 2D grid of I stick
+  // blocks x K plane chunks. Both exchange buffers are laid out chunk-major
+  // (chunk k is one contiguous block per peer), and inside a block the rows are
+  // sticks, so message (i, k) to or from a peer is one contiguous byte range on
+  // both sides. Backward: the z stage runs per stick block; the messages of
+  // block i leave as soon as z(i) is done (overlapping z(i+1)); the last
+  // block's messages go out chunk by chunk and the y/x stages of chunk k start
+  // once chunk k has arrived. Forward is the mirror image: x/y per chunk, chunk
+  // k leaves when its y stage is done, the last chunk goes out block by block
+  // and z(i) starts once block i has arrived. Every exchange runs on the data
+  // plane's channel stream (RCCL: one per process, in host call order), handed
+  // off by one event per step: a rank with T transforms uses T + 1 streams.
+  struct ExchangeStep {
+    std::vector<Transfer> xs;  // transfer list of the step (backward direction)
+    int readyKind, readyIdx;   // event the step waits for: 0 none, 1 zEv_[i], 2 chunkEv_[k]
+    int doneKind, doneIdx;     // event recorded after it: 0 none, 2 chunkEv_[k], 3 blockEv_[i]
   };
-  int exchChunks_ = 1;
+  int exchChunks_ = 1;   // K
+  int stickBlocks_ = 1;  // I
+  bool pipelined() const { return exchChunks_ > 1 || stickBlocks_ > 1; }
   double chunkModel_ = 0;  // per-peer bytes of one exchange (chunk model input)
   std::vector<int> planeBounds_;  // K+1 local plane bounds of the chunks
-  std::vector<ChunkXfer> chunks_;
+  std::vector<int> stickBounds_;  // I+1 local stick bounds of the z launches
+  std::vector<ExchangeStep> bwdSteps_, fwdSteps_;
   std::vector<std::unique_ptr<DeviceBuffer>> colBaseChunk_;  // y-stage entry bases per chunk
-  std::unique_ptr<GpuStream> commStream_;
-  std::vector<std::unique_ptr<GpuEvent>> chunkEvents_;
-  std::unique_ptr<GpuEvent> commDone_, zDone_;
+  std::vector<std::unique_ptr<GpuEvent>> zEv_, chunkEv_, blockEv_;
+  hipEvent_t step_event(int kind, int idx) const;
+  void run_steps(const std::vector<ExchangeStep>& steps, bool backward);
   // GPU-side stage timing (SPFFT_TIMING=1): timing events recorded on the
   // execution stream at the stage boundaries of each direction; the intervals
   // go into the timing tree as gpu/<direction>/<stage> once they completed.
@@ -208,7 +223,13 @@ private:
     std::vector<StageMark> marks;
   };
   std::vector<StageTrace> traces_;
+  struct ExchangeSpan {
+    const char* dir;
+    std::unique_ptr<GpuEvent> begin, end;
+  };
+  std::vector<ExchangeSpan> spans_;  // pipelined exchanges (gpu/<dir>/exchange-span)
   std::vector<std::unique_ptr<GpuEvent>> spareEvents_;
+  std::unique_ptr<GpuEvent> timing_event();
   void stage_mark(const char* dir, const char* stage);
   // records the end mark of a stage when the stage function returns
   struct StageEnd {

@@ -72,18 +72,24 @@ DeviceGuard::~DeviceGuard() {
   if (switched_) (void)hipSetDevice(previous_);
 }
 
+namespace {
+std::atomic<int> gLiveStreams{0};
+}
 GpuStream::GpuStream(bool highPriority) {
   int lo = 0, hi = 0;
   if (highPriority && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
     gpu_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreate");
-    return;
+  } else {
+    (void)hipGetLastError();
+    gpu_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
   }
-  (void)hipGetLastError();
-  gpu_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  ++gLiveStreams;
 }
 GpuStream::~GpuStream() {
+  if (stream_) --gLiveStreams;
   if (stream_ && !process_exiting()) (void)hipStreamDestroy(stream_);
 }
+int GpuStream::live() { return gLiveStreams.load(); }
 
 GpuEvent::GpuEvent(bool timing) {
   gpu_check(hipEventCreateWithFlags(&event_, timing ? hipEventDefault : hipEventDisableTiming),

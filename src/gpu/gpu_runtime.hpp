@@ -48,6 +48,11 @@ public:
   GpuStream(const GpuStream&) = delete;
   GpuStream& operator=(const GpuStream&) = delete;
   hipStream_t get() const { return stream_; }
+  // HIP streams the library currently owns (private transform streams, RCCL
+  // channel streams): with GPU_MAX_HW_QUEUES = 4, every stream beyond the
+  // queue count shares a hardware queue with another one and serialises
+  // behind it.
+  static int live();
 
 private:
   hipStream_t stream_ = nullptr;

@@ -40,16 +40,37 @@ bool mpi_finalized() {
   return f != 0;
 }
 
+// Ordering domain of a user communicator (Communicator::channel_domain): a
+// process-unique id cached on the communicator as an MPI attribute, so every
+// grid built from the same communicator gets the same id, and a communicator
+// created after another was freed (even under a recycled handle) a new one.
+unsigned long long domain_of(MPI_Comm comm) {
+  static int keyval = MPI_KEYVAL_INVALID;
+  static unsigned long long next = 0;
+  if (keyval == MPI_KEYVAL_INVALID)
+    mpi_check(MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, MPI_COMM_NULL_DELETE_FN, &keyval, nullptr));
+  void* v = nullptr;
+  int found = 0;
+  mpi_check(MPI_Comm_get_attr(comm, keyval, &v, &found));
+  if (found) return static_cast<unsigned long long>(reinterpret_cast<std::uintptr_t>(v));
+  const unsigned long long id = ++next;
+  mpi_check(MPI_Comm_set_attr(comm, keyval, reinterpret_cast<void*>(static_cast<std::uintptr_t>(id))));
+  return id;
+}
+
 }  // namespace
 
 class MpiCommunicator : public Communicator {
 public:
   // Duplicates `comm` (private message space per grid, reference
   // mpi_communicator_handle.hpp:48-66).
-  explicit MpiCommunicator(MPI_Comm comm) {
+  explicit MpiCommunicator(MPI_Comm comm) : MpiCommunicator(comm, 0) {}
+  // `domain` 0: the ordering domain of the user communicator `comm`
+  MpiCommunicator(MPI_Comm comm, unsigned long long domain) {
     int init = 0;
     MPI_Initialized(&init);
     if (!init) throw MPISupportError();
+    domain_ = domain ? domain : domain_of(comm);
     mpi_check(MPI_Comm_dup(comm, &comm_));
     mpi_check(MPI_Comm_rank(comm_, &rank_));
     mpi_check(MPI_Comm_size(comm_, &size_));
@@ -140,11 +161,13 @@ public:
   void barrier() override { mpi_check(MPI_Barrier(comm_)); }
 
   std::shared_ptr<Communicator> duplicate() const override {
-    return std::make_shared<MpiCommunicator>(comm_);
+    return std::make_shared<MpiCommunicator>(comm_, domain_);
   }
+  unsigned long long channel_domain() const override { return domain_; }
 
 private:
   MPI_Comm comm_ = MPI_COMM_NULL;
+  unsigned long long domain_ = 0;
   int rank_ = 0, size_ = 1;
 };
 

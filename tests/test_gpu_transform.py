@@ -454,19 +454,22 @@ def test_user_stream_async(gpu):
     assert (out - vals).abs().max().item() < 1e-12
 
 
-@pytest.mark.parametrize("chunks,exchange", [(1, "COMPACT_BUFFERED"), (3, "COMPACT_BUFFERED"),
-                                             (8, "COMPACT_BUFFERED"),
-                                             (3, "COMPACT_BUFFERED_FLOAT"), (3, "BUFFERED")])
+@pytest.mark.parametrize("chunks,exchange,blocks", [
+    (1, "COMPACT_BUFFERED", 1), (3, "COMPACT_BUFFERED", 1), (8, "COMPACT_BUFFERED", 1),
+    (3, "COMPACT_BUFFERED_FLOAT", 1), (3, "BUFFERED", 1), (1, "COMPACT_BUFFERED", 2),
+    (2, "COMPACT_BUFFERED", 2), (2, "BUFFERED", 4), (4, "COMPACT_BUFFERED_FLOAT", 2)])
 @pytest.mark.parametrize("dist", ["uniform", "rank0", "rank0_planes_last", "r2c"])
-def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, exchange, monkeypatch):
+def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, exchange, blocks, monkeypatch):
     """Reference distribution sweep (tests/mpi_tests/test_transform.cpp) on P=3 virtual
-    ranks of one GPU, through the plane-chunk pipelined exchange with 1, 3 and 8 chunks
-    (ranks with few or no planes get empty chunks; every rank issues the same rounds),
-    also with fp32 exchange buffers and the padded BUFFERED layout (never chunked)."""
+    ranks of one GPU, through the pipelined exchange's 2D grid of stick blocks x plane
+    chunks (1..8 chunks, 1..4 stick blocks; ranks with few or no planes or sticks get
+    empty messages and every rank issues the same steps), also with fp32 exchange
+    buffers and the padded BUFFERED layout."""
     import torch
     from spfft_amd.parallel import run_ranks
     from spfft_amd.utils.indices import calculate_num_local_xy_planes
     monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    monkeypatch.setenv("SPFFT_EXCH_STICK_BLOCKS", str(blocks))
     dims = (20, 18, 17)
     nx, ny, nz = dims
     P = 3
@@ -753,8 +756,9 @@ def test_long_lines(gpu, dims, single, ttype):
 
 @pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "COMPACT_BUFFERED_FLOAT", "BUFFERED",
                                       "BUFFERED_FLOAT", "UNBUFFERED"])
-@pytest.mark.parametrize("P,chunks", [(8, 1), (8, 2), (8, 4), (4, 3), (2, 4)])
-def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, exchange, monkeypatch):
+@pytest.mark.parametrize("P,chunks,blocks", [(8, 1, 1), (8, 2, 1), (8, 4, 1), (4, 3, 1), (2, 4, 1),
+                                             (8, 2, 2), (4, 2, 4), (2, 1, 2)])
+def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, blocks, exchange, monkeypatch):
     """The driver's scaling configurations (2/4/8 ranks, the chunk counts the automatic
     rule picks at 256^3) on virtual ranks of one GPU, with a sphere split evenly like
     bench.py, for every exchange type (BUFFERED chunks are padded blocks; UNBUFFERED
@@ -764,6 +768,7 @@ def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, exchange, monkeypatch):
     from spfft_amd.parallel import TorchDistComm, make_distributed, run_ranks  # noqa: F401
     from spfft_amd.utils.indices import distribute_sticks
     monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    monkeypatch.setenv("SPFFT_EXCH_STICK_BLOCKS", str(blocks))
     dims = (48, 40, 64)
     nx, ny, nz = dims
     gidx = sphere_indices(*dims, 0.5)
@@ -804,18 +809,20 @@ def test_gpu_virtual_ranks_scale_configs(gpu, P, chunks, exchange, monkeypatch):
 # counts and displacements). RCCL refuses two ranks of one communicator on one
 # device (profiles/r3/rccl_duplicate_device.txt), so this is how the RCCL data
 # path runs on the one-GPU box.
-@pytest.mark.parametrize("exchange,chunks", [("COMPACT_BUFFERED", 1), ("COMPACT_BUFFERED", 2),
-                                             ("COMPACT_BUFFERED", 4), ("COMPACT_BUFFERED_FLOAT", 1),
-                                             ("COMPACT_BUFFERED_FLOAT", 3), ("BUFFERED", 1),
-                                             ("BUFFERED", 2), ("BUFFERED_FLOAT", 1),
-                                             ("UNBUFFERED", 1), ("UNBUFFERED", 2)])
+@pytest.mark.parametrize("exchange,chunks,blocks", [
+    ("COMPACT_BUFFERED", 1, 1), ("COMPACT_BUFFERED", 2, 1), ("COMPACT_BUFFERED", 4, 1),
+    ("COMPACT_BUFFERED_FLOAT", 1, 1), ("COMPACT_BUFFERED_FLOAT", 3, 1), ("BUFFERED", 1, 1),
+    ("BUFFERED", 2, 1), ("BUFFERED_FLOAT", 1, 1), ("UNBUFFERED", 1, 1), ("UNBUFFERED", 2, 1),
+    ("COMPACT_BUFFERED", 2, 2), ("COMPACT_BUFFERED", 2, 4), ("BUFFERED", 2, 2),
+    ("COMPACT_BUFFERED_FLOAT", 1, 2)])
 @pytest.mark.parametrize("P", [3, 8])
-def test_gpu_virtual_ranks_rccl(gpu, P, exchange, chunks, monkeypatch):
+def test_gpu_virtual_ranks_rccl(gpu, P, exchange, chunks, blocks, monkeypatch):
     import torch
     from spfft_amd.parallel import make_distributed, run_ranks
     from spfft_amd.utils.indices import distribute_sticks
     monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
     monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    monkeypatch.setenv("SPFFT_EXCH_STICK_BLOCKS", str(blocks))
     dims = (24, 20, 18) if P == 3 else (32, 28, 40)
     gidx = sphere_indices(*dims, 0.5)
     rng = np.random.default_rng(31 + P)

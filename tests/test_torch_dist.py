@@ -2,12 +2,13 @@
 plane, one OS process per rank), the same launch path bench.py uses.
 
 CPU: host transforms, every exchange type, 2 and 3 ranks.
-GPU: 2-3 ranks sharing the box's single MI355X. RCCL refuses two ranks of one
-communicator on one device (profiles/r3/rccl_duplicate_device.txt), so these
-runs move data with the IPC peer-write plane; the RCCL initialisation-failure
-agreement and fallback are covered by fault injection. The RCCL send/recv data
-path itself runs in tests/test_gpu_transform.py (test_gpu_virtual_ranks_rccl,
-RCCL self-loopback per virtual rank).
+GPU: 2-4 ranks sharing the box's single MI355X. RCCL refuses two ranks of one
+host on one device (profiles/r3/rccl_duplicate_device.txt): by default such
+ranks move data with the IPC peer-write plane; with SPFFT_RCCL_VIRTUAL_HOSTS=1
+every rank claims its own host id and the ranks run one multi-rank RCCL
+communicator over RCCL's socket transport (test_torch_dist_rccl_multirank,
+test_bench_driver_launch_2ranks_rccl). The RCCL initialisation-failure
+agreement and fallback are covered by fault injection.
 """
 import os
 import socket
@@ -65,6 +66,23 @@ def test_torch_dist_ipc_3ranks_repeated(gpu):
     # many back-to-back transforms with fresh data: a stale read of an earlier
     # exchange (missing barrier / visibility) shows as a mismatch
     _launch(3, "UNBUFFERED", "--iters=12", "--dims=64,60,48", expect="ipc")
+
+
+# Ranks sharing the box's single GPU through ONE multi-rank RCCL communicator:
+# SPFFT_RCCL_VIRTUAL_HOSTS=1 gives every rank a host id of its own (RCCL's
+# duplicate-device check is per host), so the ranks talk over RCCL's socket
+# transport on loopback. This runs RcclDeviceComm, the class that moves the
+# data between distinct GPUs on an 8-GPU node (peer ids, staggered send/recv
+# order, grouped calls, channel stream hand-offs), through the pipelined 2D
+# grid of stick blocks x plane chunks.
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc,exchange,chunks,blocks", [
+    (2, "COMPACT_BUFFERED", 1, 1), (2, "COMPACT_BUFFERED", 2, 2), (3, "BUFFERED_FLOAT", 1, 1),
+    (3, "COMPACT_BUFFERED_FLOAT", 4, 2), (4, "BUFFERED", 2, 2), (4, "COMPACT_BUFFERED", 1, 3)])
+def test_torch_dist_rccl_multirank(gpu, monkeypatch, nproc, exchange, chunks, blocks):
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", str(chunks))
+    monkeypatch.setenv("SPFFT_EXCH_STICK_BLOCKS", str(blocks))
+    _launch(nproc, exchange, "--iters=3", "--rccl-net", expect="rccl", timeout=240)
 
 
 @pytest.mark.gpu
@@ -126,11 +144,65 @@ def test_bench_driver_launch_2ranks(gpu):
     # the reported round-trip error is the MAX over both ranks
     assert rec["config"]["check_error"]["ranks_checked"] == 2
     assert rec["config"]["check_error"]["roundtrip"] < 1e-12
+    assert rec["config"]["check_error"]["ok"]
     # both ranks ran on the one card of the test box: flagged as a rehearsal
     import torch
     ndev = torch.cuda.device_count()
     assert rec["config"]["distinct_devices"] == min(2, ndev)
     assert rec["config"]["shared_device"] is (ndev < 2)
+
+
+@pytest.mark.gpu
+def test_bench_driver_launch_2ranks_rccl(gpu, monkeypatch):
+    """The driver's multi-GPU launch line with the RCCL data plane between the two
+    ranks (virtual hosts on one device): the record carries a passing on-GPU
+    round-trip check from both ranks, per-direction stage times and the exchange
+    rate, without --check."""
+    monkeypatch.setenv("SPFFT_RCCL_VIRTUAL_HOSTS", "1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--size", "64", "--transforms", "2"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    rec = _bench_json(r.stdout)
+    cfg = rec["config"]
+    assert cfg["data_plane"] == "rccl"
+    chk = cfg["check_error"]
+    assert chk["ranks_checked"] == 2 and chk["ok"] and chk["roundtrip"] < 1e-12
+    for d in ("backward", "forward"):
+        assert cfg["stage_ms"][d]["z"] > 0
+        assert cfg["exchange"]["ms"][d] > 0 and cfg["exchange"]["GBps_per_rank"][d] > 0
+    assert "64^3" in rec["metric"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("queues", [1, 2])
+def test_bench_rccl_few_hw_queues(gpu, monkeypatch, queues):
+    """T = 4 transforms per rank on per-transform streams with K = 2 plane chunks and
+    2 stick blocks, every exchange on the process's one RCCL channel stream (T + 1
+    streams), with only 1 or 2 hardware queues per process: streams that share a
+    queue serialise in issue order, which must never put a wait in front of the
+    work it waits for."""
+    monkeypatch.setenv("SPFFT_RCCL_VIRTUAL_HOSTS", "1")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", str(queues))
+    monkeypatch.setenv("SPFFT_EXCH_CHUNKS", "2")
+    monkeypatch.setenv("SPFFT_EXCH_STICK_BLOCKS", "2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--size", "64", "--transforms", "4", "--streams", "per-transform"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    rec = _bench_json(r.stdout)
+    cfg = rec["config"]
+    assert cfg["data_plane"] == "rccl" and cfg["check_error"]["ok"], cfg
+    # the transforms run on the 4 torch streams; the library owns only the channel stream
+    assert cfg["library_streams"] == 1, cfg
 
 
 @pytest.mark.gpu

@@ -30,6 +30,11 @@ def main():
     exch_name = args[0] if args else "COMPACT_BUFFERED"
     exchange = getattr(sp.ExchangeType, exch_name)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if "--rccl-net" in sys.argv:
+        # ranks sharing one GPU through a real multi-rank RCCL communicator (one
+        # virtual host per rank, RCCL socket transport on loopback): the
+        # RcclDeviceComm path that ships to 8 GPUs, end to end
+        os.environ["SPFFT_RCCL_VIRTUAL_HOSTS"] = "1"
     pu = sp.ProcessingUnit.HOST if host else sp.ProcessingUnit.GPU
     dev = "cuda"
     if not host:
