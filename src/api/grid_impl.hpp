@@ -20,6 +20,20 @@ class DeviceComm;     // gpu/device_comm.hpp
 // Largest row/stick padding (elements) a transform may add to its buffers.
 constexpr int kMaxPad = 32;
 
+// Row padding (elements) of the GPU stick rows and intermediate rows: n + pad
+// elements of elemBytes make an odd multiple of 128 bytes, so every row starts
+// on a cache line (a row that starts mid-line costs a partial line at each end:
+// fp32 rows of 256 + 8 elements made the y and x stages read 1.5x their bytes,
+// TCC_EA0_RDREQ in profiles/r4/pmc) and consecutive rows do not share a
+// 256-byte channel stride. Short rows (< 1 KB) keep a pad of 8.
+inline int aligned_row_pad(int n, int elemBytes) {
+  const int line = 128 / elemBytes;
+  if (static_cast<long long>(n) * elemBytes < 1024 || line < 1) return 8;
+  for (int p = 0; p <= kMaxPad; ++p)
+    if ((n + p) % line == 0 && ((n + p) / line) % 2 == 1) return p;
+  return 8;
+}
+
 template <typename T>
 class GridImpl {
 public:

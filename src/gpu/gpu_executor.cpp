@@ -42,10 +42,12 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   DeviceGuard guard(deviceId_);
   const IndexPlan& p = *plan_;
   const bool distributed = p.size > 1;
-  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()),
-                                 env_int("SPFFT_PAD_STICK", 8, 0, kMaxPad));
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
-  interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", 8, 0, kMaxPad);
+  const int stickElemBytes = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
+  layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()),
+                                 env_int("SPFFT_PAD_STICK", aligned_row_pad(p.dimZ, stickElemBytes), 0,
+                                         kMaxPad));
+  interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", aligned_row_pad(p.dimY, sizeof(cx<T>)), 0, kMaxPad);
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
   // launches in stream-ordered use (profiles/README.md, session 6)

@@ -41,6 +41,7 @@ struct ZArgs {
   const int* runOffsets;
   const StickDesc* desc;     // non-null when every stick is simple (fast path)
   int single;                // 1: exchange side is the plain [S][stickStride] array
+                             // (2: distributed, segment table read from global memory)
   long long stickStride;     // element stride between sticks when single
   // otherwise, per plane z two entries: (base, stride) of its exchange segment,
   // element (stick s, plane z) at base + s * stride (base includes z)

@@ -459,7 +459,7 @@ struct SegMap {
   __device__ explicit SegMap(const ZArgs& a)
       : single(pin_uniform(a.single)), stride(pin_uniform64(a.stickStride)), tab(a.zTab) {}
   __device__ long long at(int s, int pos) const {
-    if (single) return static_cast<long long>(s) * stride + pos;
+    if (single == 1) return static_cast<long long>(s) * stride + pos;
     using V = long long __attribute__((ext_vector_type(2)));
     const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
     return t.x + static_cast<long long>(s) * t.y;
@@ -601,22 +601,30 @@ __device__ __forceinline__ int find_run(const RunTable& t, int idx) {
 // the z forward kernel a third of its workgroups per CU (66 -> 73 us), as did
 // computing a single rank's table in LDS. (A kernel template per plan kind
 // doubled the z kernels and tripled their compile time.)
+// Distributed launches whose engine leaves no room for the table (long z lines
+// near the LDS limit) read it from global memory instead (ZArgs::single = 2,
+// set by the launcher: z_args_for_lds).
 struct ZSeg {
   int single;
   long long stride;
-  const long long* tab;  // LDS (distributed plans)
+  const long long* tab;   // LDS (distributed plans)
+  const long long* gtab;  // global memory (single == 2)
   __device__ ZSeg(const ZArgs& a, char* ldsTab, int n)
       : single(pin_uniform(a.single)), stride(pin_uniform64(a.stickStride)),
-        tab(reinterpret_cast<const long long*>(ldsTab)) {
-    if (!single) {
+        tab(reinterpret_cast<const long long*>(ldsTab)), gtab(a.zTab) {
+    if (single == 0) {
       long long* t = reinterpret_cast<long long*>(ldsTab);
       for (int i = threadIdx.x; i < 2 * n; i += blockDim.x) t[i] = a.zTab[i];
       __syncthreads();
     }
   }
   __device__ long long at(int s, int pos) const {
-    if (single) return static_cast<long long>(s) * stride + pos;
     using V = long long __attribute__((ext_vector_type(2)));
+    if (single == 1) return static_cast<long long>(s) * stride + pos;
+    if (single == 2) {
+      const V t = *reinterpret_cast<const V*>(gtab + 2 * pos);
+      return t.x + static_cast<long long>(s) * t.y;
+    }
     const V t = *reinterpret_cast<const V*>(tab + 2 * pos);
     return t.x + static_cast<long long>(s) * t.y;
   }
@@ -627,6 +635,15 @@ __host__ __device__ constexpr std::size_t zseg_lds_offset(std::size_t fftBytes, 
 }
 inline std::size_t zseg_lds_bytes(const ZArgs& a) {
   return a.single ? 0 : std::size_t(2) * a.n * sizeof(long long) + 16;
+}
+// The launch's arguments and LDS bytes: a distributed plan's segment table
+// moves to global memory when it would push the workgroup past the LDS limit.
+inline ZArgs z_args_for_lds(const ZArgs& a, std::size_t fftBytes, int lines, std::size_t* ldsTotal) {
+  ZArgs b = a;
+  constexpr std::size_t kLimit = 160 * 1024;
+  if (!b.single && zseg_lds_offset(fftBytes, lines) + zseg_lds_bytes(b) > kLimit) b.single = 2;
+  *ldsTotal = zseg_lds_offset(fftBytes, lines) + zseg_lds_bytes(b);
+  return b;
 }
 
 // Workgroup -> tile mapping: the dispatcher deals consecutive workgroups

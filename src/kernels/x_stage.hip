@@ -81,11 +81,9 @@ RtPlan make_rt_plan_from(int n, std::size_t elemBytes, const std::vector<int>& r
   const std::size_t regions = p.inplace ? 1 : 2;
   if (regions * static_cast<std::size_t>(n + 1) * elemBytes > 160 * 1024) throw GPUFFTError();
   // Lines: a power of two (line-fast engines split lane indices with shifts).
-  // Line stride: the passes run lines fastest, so consecutive lines start
-  // kMod / lines bank slots apart (an odd stride when lines >= kMod): a wave's
-  // accesses to one position of all lines hit distinct 16-B (fp64) / 8-B
-  // (fp32) slots of the 256-byte bank row.
-  const int kMod = static_cast<int>(256 / elemBytes);
+  // Line stride: the passes run lines fastest, so a 16-lane LDS access group
+  // spans lines; lds_line_stride_ok puts them on distinct bank slots (the rule
+  // of the compile-time line-fast engines, fft_device.hpp).
   int lines = static_cast<int>(budget / (regions * static_cast<std::size_t>(n + 1) * elemBytes));
   if (lines > kMaxThreads) lines = kMaxThreads;
   if (lines < 1) lines = 1;
@@ -95,9 +93,8 @@ RtPlan make_rt_plan_from(int n, std::size_t elemBytes, const std::vector<int>& r
     while (p.linesLog2 > 0 && !fits(p.linesLog2)) --p.linesLog2;
   for (;;) {
     p.lines = 1 << p.linesLog2;
-    const int want = p.lines >= kMod ? 1 : kMod / p.lines;
     p.ls = n;
-    while (p.ls % kMod != want % kMod) ++p.ls;
+    while (!lds_line_stride_ok(p.ls, p.lines, static_cast<int>(elemBytes))) ++p.ls;
     if (p.linesLog2 == 0 || regions * p.lines * static_cast<std::size_t>(p.ls) * elemBytes <= budget)
       break;
     --p.linesLog2;

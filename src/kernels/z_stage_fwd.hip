@@ -12,9 +12,10 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     using E = decltype(eng);
     auto k = a.desc ? z_forward_desc_kernel<E, T, BT> : z_forward_kernel<E, T, BT>;
-    const std::size_t ldsTotal = zseg_lds_offset(lds, lines) + zseg_lds_bytes(a);
+    std::size_t ldsTotal = 0;
+    const ZArgs b = z_args_for_lds(a, lds, lines, &ldsTotal);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
+    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, b,
                        in, values, scale, tw);
     gpu_check_launch("z_forward", stream);
   });

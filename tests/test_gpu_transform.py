@@ -279,6 +279,39 @@ def test_gpu_virtual_ranks(gpu, exchange):
         assert e1 < tol and e2 < tol
 
 
+@pytest.mark.parametrize("exchange", ["COMPACT_BUFFERED", "BUFFERED"])
+@pytest.mark.parametrize("nz", [4000, 5000])
+def test_gpu_virtual_ranks_z_near_lds_limit(gpu, exchange, nz):
+    """Distributed plan whose z engine nearly fills the 160 KB LDS (fp64 run-time
+    engine, dimZ 4000 / 5000): the per-plane exchange segment table no longer fits
+    next to it and is read from global memory instead (z_args_for_lds)."""
+    import torch
+    from spfft_amd.parallel import make_distributed, run_ranks
+    from spfft_amd.utils.indices import distribute_sticks
+    dims = (6, 5, nz)
+    gidx = sphere_indices(*dims, 0.5)
+    rng = np.random.default_rng(19)
+    vals = _rand_vals(rng, len(gidx))
+    ref = dense_backward(gidx, vals, dims)
+    P = 2
+    parts = distribute_sticks(gidx, P, dims)
+    ex = getattr(sp.ExchangeType, exchange)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        s = make_distributed(comm, dims, gidx, processing_unit=GPU, exchange_type=ex)
+        start = sum(len(p) for p in parts[:rank])
+        v = torch.as_tensor(vals[start:start + len(s.indices)], device="cuda")
+        out = s.transform.backward(v).cpu().numpy()
+        e1 = max_rel_error(out, ref[s.z_offset:s.z_offset + s.z_length])
+        f = s.transform.forward(None, scaling=sp.Scaling.FULL).cpu().numpy()
+        e2 = max_rel_error(f, v.cpu().numpy())
+        return e1, e2
+
+    for e1, e2 in run_ranks(P, body):
+        assert e1 < 1e-11 and e2 < 1e-11
+
+
 def test_multi_transform_gpu(gpu):
     import torch
     rng = np.random.default_rng(12)
