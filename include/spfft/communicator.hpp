@@ -29,6 +29,15 @@ public:
   virtual void wait() = 0;
 };
 
+/* One peer's part of an alltoallw (SpFFT-AMD): `count` blocks of `blockBytes`
+ * bytes, `strideBytes` apart, starting at byte `offset` of the buffer. */
+struct StridedLayout {
+  std::size_t offset;
+  std::size_t count;
+  std::size_t blockBytes;
+  std::size_t strideBytes;
+};
+
 class SPFFT_EXPORT Communicator {
 public:
   virtual ~Communicator();
@@ -52,6 +61,20 @@ public:
                                                       const std::size_t* sendDispls, void* recv,
                                                       const std::size_t* recvCounts,
                                                       const std::size_t* recvDispls);
+
+  /* All-to-all between strided layouts (one per rank on each side), with no
+   * intermediate copy where the transport supports it: the MPI communicator
+   * runs MPI_Alltoallw with hvector datatypes, the reference's UNBUFFERED
+   * exchange (src/transpose/transpose_mpi_unbuffered_host.cpp:66-181). The
+   * default packs into temporary buffers around alltoallv(). */
+  virtual void alltoallw(const void* send, const StridedLayout* sendLayouts, void* recv,
+                         const StridedLayout* recvLayouts);
+  /* Non-blocking alltoallw (MPI_Ialltoallw); the layout arrays may be released on
+   * return. The default runs alltoallw() at once. */
+  virtual std::unique_ptr<ExchangeRequest> ialltoallw(const void* send,
+                                                      const StridedLayout* sendLayouts,
+                                                      void* recv,
+                                                      const StridedLayout* recvLayouts);
 
   virtual void barrier();
 

@@ -1,3 +1,4 @@
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -22,6 +23,37 @@ std::unique_ptr<ExchangeRequest> Communicator::ialltoallv(const void* send, cons
                                                           const std::size_t* rc,
                                                           const std::size_t* rd) {
   alltoallv(send, sc, sd, recv, rc, rd);
+  return std::unique_ptr<ExchangeRequest>(new CompletedRequest());
+}
+
+void Communicator::alltoallw(const void* send, const StridedLayout* sl, void* recv,
+                             const StridedLayout* rl) {
+  const int P = size();
+  std::vector<std::size_t> sc(P), sd(P), rc(P), rd(P);
+  std::size_t st = 0, rt = 0;
+  for (int r = 0; r < P; ++r) {
+    sc[r] = sl[r].count * sl[r].blockBytes;
+    sd[r] = st;
+    st += sc[r];
+    rc[r] = rl[r].count * rl[r].blockBytes;
+    rd[r] = rt;
+    rt += rc[r];
+  }
+  std::vector<char> sbuf(std::max<std::size_t>(st, 1)), rbuf(std::max<std::size_t>(rt, 1));
+  for (int r = 0; r < P; ++r)
+    for (std::size_t b = 0; b < sl[r].count; ++b)
+      std::memcpy(sbuf.data() + sd[r] + b * sl[r].blockBytes,
+                  static_cast<const char*>(send) + sl[r].offset + b * sl[r].strideBytes, sl[r].blockBytes);
+  alltoallv(sbuf.data(), sc.data(), sd.data(), rbuf.data(), rc.data(), rd.data());
+  for (int r = 0; r < P; ++r)
+    for (std::size_t b = 0; b < rl[r].count; ++b)
+      std::memcpy(static_cast<char*>(recv) + rl[r].offset + b * rl[r].strideBytes,
+                  rbuf.data() + rd[r] + b * rl[r].blockBytes, rl[r].blockBytes);
+}
+
+std::unique_ptr<ExchangeRequest> Communicator::ialltoallw(const void* send, const StridedLayout* sl,
+                                                          void* recv, const StridedLayout* rl) {
+  alltoallw(send, sl, recv, rl);
   return std::unique_ptr<ExchangeRequest>(new CompletedRequest());
 }
 

@@ -7,10 +7,14 @@
 // the results) with contiguous W-element runs wherever the layout allows, so
 // the gathers are cache-line sized. Replaces FFTW's plan-many batches of the
 // reference host path (reference: src/fft/transform_1d_host.hpp:49-130,
-// fftw_plan_1d.hpp:46-166); lengths with a prime factor above kBluesteinPrime
-// keep the scalar Bluestein engine (HostFft) line by line.
+// fftw_plan_1d.hpp:46-166). Lengths with a prime factor above kBluesteinPrime
+// run Bluestein's chirp-z convolution on W lines at once: two batched
+// power-of-two FFTs of length m >= 2n-1 with the chirp and filter products in
+// between, in a per-thread scratch buffer that is reused across calls.
 #pragma once
 
+#include <cmath>
+#include <memory>
 #include <utility>
 #include <vector>
 
@@ -55,25 +59,201 @@ public:
 
   HostFftBatch() = default;
   explicit HostFftBatch(int n) : n_(n), radices_(stockham_radices(n)), tw_(make_twiddles<T>(n)) {
-    batched_ = n <= 1 || radices_.empty() || radices_.back() <= kBluesteinPrime;
-    if (!batched_) scalar_ = HostFft<T>(n);
+    if (n > 1 && !radices_.empty() && radices_.back() > kBluesteinPrime) {
+      if (!init_rader()) init_bluestein();
+    }
   }
 
   int size() const { return n_; }
-  // false: the length needs Bluestein; run scalar() line by line instead
-  bool batched() const { return batched_; }
-  const HostFft<T>& scalar() const { return scalar_; }
+  // every length runs batched (Bluestein lengths through the chirp-z path)
+  bool batched() const { return true; }
+  bool bluestein() const { return static_cast<bool>(blue_); }
+  bool rader() const { return static_cast<bool>(rader_); }
 
   // In-place transform of the W lines held in a[0..n); b is scratch of n
   // elements. sign +1: exp(+2 pi i jk/n) (backward), -1: forward.
   void run(VC* a, VC* b, int sign) const {
     if (n_ <= 1) return;
+    if (rader_) {
+      rader_run(a, sign);
+      return;
+    }
+    if (blue_) {
+      bluestein_run(a, sign);
+      return;
+    }
     const VC* res = sign > 0 ? passes<+1>(a, b) : passes<-1>(a, b);
     if (res != a)
       for (int i = 0; i < n_; ++i) a[i] = res[i];
   }
 
 private:
+  // Bluestein: jk = (j^2 + k^2 - (k-j)^2) / 2, so with c_j = exp(S i pi j^2 / n)
+  // X_k = c_k sum_j (x_j c_j) conj(c_{k-j}): a circular convolution of length
+  // m >= 2n-1 (power of two) through the batched engine; the filter spectra
+  // (one per sign) are computed once.
+  struct Blue {
+    int m = 0;
+    std::shared_ptr<const HostFftBatch> inner;
+    std::vector<cx<T>> chirp;       // c_j for S = -1
+    std::vector<cx<T>> filter[2];   // [0]: S = -1, [1]: S = +1
+  };
+  void init_bluestein() {
+    auto b = std::make_shared<Blue>();
+    int m = 1;
+    while (m < 2 * n_ - 1) m *= 2;
+    b->m = m;
+    b->inner = std::make_shared<const HostFftBatch>(m);
+    b->chirp.resize(n_);
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int j = 0; j < n_; ++j) {
+      const long long q = (static_cast<long long>(j) * j) % (2LL * n_);  // exact phase reduction
+      const long double ang = pi * static_cast<long double>(q) / static_cast<long double>(n_);
+      b->chirp[j] = mk<T>(static_cast<T>(std::cos(ang)), static_cast<T>(-std::sin(ang)));
+    }
+    std::vector<VC> work(2 * static_cast<std::size_t>(m));
+    for (int s = 0; s < 2; ++s) {
+      VC* f = work.data();
+      for (int j = 0; j < m; ++j) f[j] = zero();
+      for (int j = 0; j < n_; ++j) {
+        const cx<T> cj = s == 0 ? b->chirp[j] : conj(b->chirp[j]);
+        f[j] = broadcast(conj(cj));
+        if (j > 0) f[m - j] = f[j];
+      }
+      b->inner->run(f, f + m, -1);
+      b->filter[s].resize(m);
+      for (int j = 0; j < m; ++j) b->filter[s][j] = lane0(f[j]);
+    }
+    blue_ = std::move(b);
+  }
+  static VC zero() {
+    VC z;
+    z.x = V(T(0));
+    z.y = V(T(0));
+    return z;
+  }
+  static VC broadcast(cx<T> v) {
+    VC r;
+    r.x = V(v.x);
+    r.y = V(v.y);
+    return r;
+  }
+  static cx<T> lane0(const VC& v) { return mk<T>(v.x[0], v.y[0]); }
+  void bluestein_run(VC* a, int sign) const {
+    const Blue& b = *blue_;
+    const int m = b.m;
+    // per-thread scratch, grown once and reused by every later call
+    thread_local std::vector<VC> tls;
+    if (tls.size() < 2 * static_cast<std::size_t>(m)) tls.resize(2 * static_cast<std::size_t>(m));
+    VC* u = tls.data();
+    const bool plus = sign > 0;
+    for (int j = 0; j < n_; ++j)
+      u[j] = plus ? twv<+1>(a[j], b.chirp[j]) : twv<-1>(a[j], b.chirp[j]);  // x_j c_j
+    for (int j = n_; j < m; ++j) u[j] = zero();
+    b.inner->run(u, u + m, -1);
+    const std::vector<cx<T>>& f = b.filter[plus ? 1 : 0];
+    for (int j = 0; j < m; ++j) u[j] = twv<-1>(u[j], f[j]);
+    b.inner->run(u, u + m, +1);
+    const T inv = T(1) / static_cast<T>(m);
+    for (int k = 0; k < n_; ++k) {
+      VC v = plus ? twv<+1>(u[k], b.chirp[k]) : twv<-1>(u[k], b.chirp[k]);
+      v.x *= inv;
+      v.y *= inv;
+      a[k] = v;
+    }
+  }
+
+  // Rader (prime n whose n - 1 has a direct Stockham plan, e.g. 101 = 4 * 25 + 1):
+  // with a generator g of the multiplicative group mod n, a_q = x_{g^q} and
+  // b_q = w^{g^-q} (w = exp(S 2 pi i / n)), X_{g^-q} = x_0 + (a (*) b)_q, a cyclic
+  // convolution of length n - 1: two batched FFTs of length n - 1 instead of
+  // Bluestein's two of length >= 2n - 1 (a power of two: 256 for 101).
+  struct Rader {
+    std::shared_ptr<const HostFftBatch> inner;
+    std::vector<int> in, out;       // g^q, g^-q mod n (q = 0 .. n-2)
+    std::vector<cx<T>> filter[2];   // FFT_{n-1}(b) / (n - 1): [0] S = -1, [1] S = +1
+  };
+  static bool is_prime(int n) {
+    if (n < 2) return false;
+    for (int d = 2; static_cast<long long>(d) * d <= n; ++d)
+      if (n % d == 0) return false;
+    return true;
+  }
+  bool init_rader() {
+    if (!is_prime(n_) || n_ < 5) return false;
+    const std::vector<int> inner = stockham_radices(n_ - 1);
+    if (inner.empty() || inner.back() > kBluesteinPrime) return false;
+    // smallest generator: g^((n-1)/f) != 1 for every prime factor f of n - 1
+    std::vector<int> fac;
+    for (int q = n_ - 1, d = 2; q > 1; ++d) {
+      if (static_cast<long long>(d) * d > q) d = q;
+      if (q % d == 0) {
+        fac.push_back(d);
+        while (q % d == 0) q /= d;
+      }
+    }
+    auto pw = [&](long long b, long long e) {
+      long long r = 1;
+      b %= n_;
+      for (; e; e >>= 1, b = b * b % n_)
+        if (e & 1) r = r * b % n_;
+      return r;
+    };
+    int g = 2;
+    for (;; ++g) {
+      bool ok = true;
+      for (int f : fac) ok = ok && pw(g, (n_ - 1) / f) != 1;
+      if (ok) break;
+    }
+    auto r = std::make_shared<Rader>();
+    const int m = n_ - 1;
+    r->inner = std::make_shared<const HostFftBatch>(m);
+    r->in.resize(m);
+    r->out.resize(m);
+    const long long ginv = pw(g, n_ - 2);
+    long long x = 1, y = 1;
+    for (int q = 0; q < m; ++q) {
+      r->in[q] = static_cast<int>(x);
+      r->out[q] = static_cast<int>(y);
+      x = x * g % n_;
+      y = y * ginv % n_;
+    }
+    std::vector<VC> work(2 * static_cast<std::size_t>(m));
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int s = 0; s < 2; ++s) {
+      VC* f = work.data();
+      for (int q = 0; q < m; ++q) {
+        const long double ang = 2 * pi * static_cast<long double>(r->out[q]) / static_cast<long double>(n_);
+        const T c = static_cast<T>(std::cos(ang)), sn = static_cast<T>(std::sin(ang));
+        f[q] = broadcast(mk<T>(c, s == 0 ? -sn : sn));
+      }
+      r->inner->run(f, f + m, -1);
+      r->filter[s].resize(m);
+      const T inv = T(1) / static_cast<T>(m);
+      for (int q = 0; q < m; ++q) r->filter[s][q] = mk<T>(f[q].x[0] * inv, f[q].y[0] * inv);
+    }
+    rader_ = std::move(r);
+    return true;
+  }
+  void rader_run(VC* a, int sign) const {
+    const Rader& r = *rader_;
+    const int m = n_ - 1;
+    thread_local std::vector<VC> tls;
+    if (tls.size() < 2 * static_cast<std::size_t>(m)) tls.resize(2 * static_cast<std::size_t>(m));
+    VC* u = tls.data();
+    VC x0 = a[0], sum = a[0];
+    for (int q = 0; q < m; ++q) {
+      u[q] = a[r.in[q]];
+      sum = sum + u[q];
+    }
+    r.inner->run(u, u + m, -1);
+    const std::vector<cx<T>>& f = r.filter[sign > 0 ? 1 : 0];
+    for (int q = 0; q < m; ++q) u[q] = twv<-1>(u[q], f[q]);
+    r.inner->run(u, u + m, +1);
+    a[0] = sum;
+    for (int q = 0; q < m; ++q) a[r.out[q]] = x0 + u[q];
+  }
+
   template <int S>
   const VC* passes(VC* a, VC* b) const {
     int ns = 1;
@@ -151,10 +331,10 @@ private:
   }
 
   int n_ = 0;
-  bool batched_ = true;
   std::vector<int> radices_;
   std::vector<cx<T>> tw_;
-  HostFft<T> scalar_;
+  std::shared_ptr<const Blue> blue_;  // immutable after construction (shared by copies)
+  std::shared_ptr<const Rader> rader_;
 };
 
 // Lane access of a batch element through its memory (re lanes then im lanes):

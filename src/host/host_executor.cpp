@@ -46,6 +46,19 @@ HostExecutor<T>::HostExecutor(std::shared_ptr<GridImpl<T>> grid,
   const bool distributed = p.size > 1;
   layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()));
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
+  unbuffered_ = distributed && grid_->exchange_type() == SPFFT_EXCH_UNBUFFERED;
+  if (unbuffered_) {
+    // UNBUFFERED: the stick side keeps the natural [stick][z] layout (the z
+    // stage writes whole sticks) and the exchange gathers each rank's planes
+    // out of it with strided datatypes (Communicator::alltoallw)
+    const i64 S = p.local_sticks();
+    for (int r = 0; r < p.size; ++r) {
+      layout_.stickDispl[r] = p.planeOffsets[r];
+      layout_.stickStride[r] = p.dimZ;
+      layout_.stickCount[r] = S * p.planesPerRank[r];
+    }
+    layout_.stickTotal = S * p.dimZ;
+  }
   if (layout_.stickTotal > grid_->slot_elements(GridImpl<T>::kStickSide) ||
       layout_.slabTotal > grid_->slot_elements(GridImpl<T>::kSlabSide))
     throw InvalidParameterError();
@@ -75,22 +88,11 @@ typename HostExecutor<T>::VC* HostExecutor<T>::scratch(int thread, std::size_t n
   return s.data();
 }
 
-// W lines of a batch through `f` (a: n batch elements, b: n scratch elements);
-// lengths without a batched plan run the scalar engine lane by lane.
+// W lines of a batch through `f` (a: n batch elements, b: n scratch elements;
+// every length runs batched, Bluestein lengths included).
 template <typename T>
-void HostExecutor<T>::fft(const Fft& f, VC* a, VC* b, int nl, int sign) {
-  if (f.batched()) {
-    f.run(a, b, sign);
-    return;
-  }
-  const int n = f.size();
-  const HostFft<T>& s = f.scalar();
-  std::vector<cx<T>> line(n), work(s.scratch_size());
-  for (int l = 0; l < nl; ++l) {
-    for (int i = 0; i < n; ++i) line[i] = lane<T>(a[i], l);
-    s.execute(line.data(), 1, line.data(), 1, sign, work.data());
-    for (int i = 0; i < n; ++i) set_lane<T>(a[i], l, line[i]);
-  }
+void HostExecutor<T>::fft(const Fft& f, VC* a, VC* b, int /*nl*/, int sign) {
+  f.run(a, b, sign);
 }
 
 // ---------------------------------------------------------------- backward
@@ -505,6 +507,10 @@ template <typename T>
 void HostExecutor<T>::exchange(bool backward, bool nonBlocking) {
   finish_exchange();
   if (plan_->size <= 1) return;
+  if (unbuffered_) {
+    exchange_strided(backward, nonBlocking);
+    return;
+  }
   const std::size_t elemBytes = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   const int P = plan_->size;
   std::vector<std::size_t> sc(P), sd(P), rc(P), rd(P);
@@ -525,6 +531,40 @@ void HostExecutor<T>::exchange(bool backward, bool nonBlocking) {
     pending_ = grid_->communicator()->ialltoallv(src, sc.data(), sd.data(), dst, rc.data(), rd.data());
   else
     grid_->communicator()->alltoallv(src, sc.data(), sd.data(), dst, rc.data(), rd.data());
+}
+
+// UNBUFFERED: rank r's planes of every local stick move straight out of (into)
+// the [stick][z] array as one strided layout (S blocks of planes(r) elements,
+// dimZ apart); the slab side holds each rank's block contiguously.
+template <typename T>
+void HostExecutor<T>::exchange_strided(bool backward, bool nonBlocking) {
+  SPFFT_TIMED_SCOPE("alltoallw");
+  const IndexPlan& p = *plan_;
+  const std::size_t eb = sizeof(cx<T>);
+  const int P = p.size;
+  const std::size_t S = static_cast<std::size_t>(p.local_sticks());
+  std::vector<StridedLayout> stickL(P), slabL(P);
+  for (int r = 0; r < P; ++r) {
+    const std::size_t planes = static_cast<std::size_t>(p.planesPerRank[r]);
+    stickL[r] = StridedLayout{static_cast<std::size_t>(p.planeOffsets[r]) * eb, planes ? S : 0, planes * eb,
+                              static_cast<std::size_t>(p.dimZ) * eb};
+    const std::size_t bytes = static_cast<std::size_t>(layout_.slabCount[r]) * eb;
+    slabL[r] = StridedLayout{static_cast<std::size_t>(layout_.slabDispl[r]) * eb, bytes ? 1u : 0u, bytes, bytes};
+  }
+  void* stick = grid_->host_slot(GridImpl<T>::kStickSide);
+  void* slab = grid_->host_slot(GridImpl<T>::kSlabSide);
+  Communicator& c = *grid_->communicator();
+  if (backward) {
+    if (nonBlocking)
+      pending_ = c.ialltoallw(stick, stickL.data(), slab, slabL.data());
+    else
+      c.alltoallw(stick, stickL.data(), slab, slabL.data());
+  } else {
+    if (nonBlocking)
+      pending_ = c.ialltoallw(slab, slabL.data(), stick, stickL.data());
+    else
+      c.alltoallw(slab, slabL.data(), stick, stickL.data());
+  }
 }
 
 template <typename T>

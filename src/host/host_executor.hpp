@@ -60,6 +60,7 @@ private:
   // x-line gathers (one element per column) do not all hit one cache set
   i64 block_stride() const { return plan_->dimY + 1; }
   void exchange(bool backward, bool nonBlocking);
+  void exchange_strided(bool backward, bool nonBlocking);
   void finish_exchange();
   std::unique_ptr<ExchangeRequest> pending_;
   void poison(bool backward);
@@ -69,6 +70,7 @@ private:
   std::shared_ptr<const IndexPlan> plan_;
   ExchangeLayout layout_;
   bool floatExchange_ = false;
+  bool unbuffered_ = false;  // UNBUFFERED: natural stick layout, strided alltoallw
   bool packedReal_ = false;  // R2C with even dimX: half-length x FFTs
   bool fuseXY_ = false;      // y/x stages fused per block of W planes
   Fft fftX_, fftY_, fftZ_;

@@ -28,27 +28,17 @@ namespace dev {
 
 constexpr int kMaxThreads = 256;
 
-#ifndef SPFFT_LDS_BUDGET
-#define SPFFT_LDS_BUDGET (64 * 1024)
-#endif
-#ifndef SPFFT_LF_MAX_LINES
-#define SPFFT_LF_MAX_LINES 16
-#endif
-// LDS per workgroup for the FFT lines (tuning knob; see tools/gpu_variants.sh)
-constexpr int kLdsBudget = SPFFT_LDS_BUDGET;
+// LDS per workgroup for the FFT lines of the default shapes
+constexpr int kLdsBudget = 64 * 1024;
+// Lines of the line-fast mapping (at most; a power of two)
+constexpr int kLfMaxLines = 16;
 // Elements per workgroup of the in-place run-time engine (lines * n): it bounds
 // the lanes' register staging (lines * n / (R * threads) butterflies per pass).
 // 4096 = 64 KB of complex<double>, 32 KB of complex<float>: the best of the
 // 32/64 KB budgets measured for each precision (profiles/README.md, session 5).
-#ifndef SPFFT_RT_ELEMS
-#define SPFFT_RT_ELEMS 4096
-#endif
-constexpr int kRtElems = SPFFT_RT_ELEMS;
-// Workgroup size of the run-time engine kernels (tuning knob).
-#ifndef SPFFT_RT_THREADS
-#define SPFFT_RT_THREADS 256
-#endif
-constexpr int kRtThreads = SPFFT_RT_THREADS;
+constexpr int kRtElems = 4096;
+// Workgroup size of the run-time engine kernels.
+constexpr int kRtThreads = 256;
 
 template <typename T>
 struct LdsGeom;
@@ -116,21 +106,10 @@ template <>
 struct CtShape<128> {
   static constexpr int E = 16, R0 = 16, R1 = 8, R2 = 1;
 };
-#ifndef SPFFT_CT256_E
-#define SPFFT_CT256_DEFAULT_SHAPE 1
-#define SPFFT_CT256_E 16
-#endif
-#if SPFFT_CT256_E == 8
-template <>
-struct CtShape<256> {
-  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4;
-};
-#else
 template <>
 struct CtShape<256> {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 1;
 };
-#endif
 template <>
 struct CtShape<512> {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8;
@@ -180,15 +159,8 @@ struct CtShapeSel : std::conditional<LF, CtShapeT<T, N>, CtShapeT<void, N>>::typ
 // N = 128 likewise (radices 8, 8, 2; 16 lanes per line): 256^3 R2C 6467 ->
 // 6820 transforms/s (packed-real x stage on N/2 = 128), 128^3 C2C 23770 ->
 // 25550 (profiles/r2_s1/shape_ab.txt)
-#ifndef SPFFT_CT128_E8
-#define SPFFT_CT128_E8 1
-#endif
 // ... and for the row-mapped forward engines of N = 128 (z forward at 128^3:
 // 14.8 -> 11.9 us, 128^3 C2C +3.6%; the row-mapped packed-real R2C x stage)
-#ifndef SPFFT_CT128F_E8
-#define SPFFT_CT128F_E8 1
-#endif
-#if SPFFT_CT128_E8
 struct CtShape128E8 {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 2, kBudget = kLdsBudget;
 };
@@ -198,31 +170,15 @@ template <>
 struct CtShapeSel<double, 128, 1, true> : CtShape128E8 {};
 template <>
 struct CtShapeSel<double, 128, -1, true> : CtShape128E8 {};
-#if SPFFT_CT128F_E8
 template <>
 struct CtShapeSel<double, 128, -1, false> : CtShape128E8 {};
-#endif
-#endif
 // Wide (512-thread) line-fast shapes for the long fp32 / fp64 lines, where the
 // default shapes leave 2 waves per SIMD under the LDS budget. Measured on
 // MI355X (profiles/r2_s1/wide_ab.txt): 512^3 R2C fp32 1400 -> 1438, 512^3 C2C
 // fp64 498 -> 511 transforms/s; for fp32 N = 256 the wide shape was slower
-// (6064 -> 5703 at 256^3 C2C fp32) and stays off.
-#ifndef SPFFT_WIDE_F512
-#define SPFFT_WIDE_F512 1
-#endif
-#ifndef SPFFT_WIDE_D512
-#define SPFFT_WIDE_D512 1
-#endif
-#ifndef SPFFT_WIDE_F256
-#define SPFFT_WIDE_F256 0
-#endif
-// measured at 1024^3 C2C fp64 (profiles/r2_s1/wide_ab.txt): 24.2 -> 47.0 transforms/s
-#ifndef SPFFT_WIDE_1024
-#define SPFFT_WIDE_1024 1
-#endif
-#if SPFFT_WIDE_1024
-// N = 1024 line-fast: with the 64 KB budget only 2 (fp64) / 8 (fp32) lines fit,
+// (6064 -> 5703 at 256^3 C2C fp32) and is not used.
+// N = 1024 (measured at 1024^3 C2C fp64, profiles/r2_s1/wide_ab.txt: 24.2 ->
+// 47.0 transforms/s) line-fast: with the 64 KB budget only 2 (fp64) / 8 (fp32) lines fit,
 // i.e. 32 / 64-byte column segments; these shapes take 8 / 16 lines (128-byte
 // segments) in one 139 KB workgroup of 512 threads per CU.
 struct CtShapeD1024W {
@@ -239,8 +195,6 @@ template <>
 struct CtShapeSel<float, 1024, 1, true> : CtShapeF1024W {};
 template <>
 struct CtShapeSel<float, 1024, -1, true> : CtShapeF1024W {};
-#endif
-#if SPFFT_WIDE_F512
 struct CtShapeF512W {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024, kMaxThr = 512;
 };
@@ -248,8 +202,6 @@ template <>
 struct CtShapeSel<float, 512, 1, true> : CtShapeF512W {};
 template <>
 struct CtShapeSel<float, 512, -1, true> : CtShapeF512W {};
-#endif
-#if SPFFT_WIDE_D512
 struct CtShapeD512W {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8, kBudget = 80 * 1024, kMaxThr = 512;
 };
@@ -257,25 +209,12 @@ template <>
 struct CtShapeSel<double, 512, 1, true> : CtShapeD512W {};
 template <>
 struct CtShapeSel<double, 512, -1, true> : CtShapeD512W {};
-#endif
-#if SPFFT_WIDE_F256
-struct CtShapeF256W {
-  static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4, kBudget = kLdsBudget, kMaxThr = 512;
-};
-template <>
-struct CtShapeSel<float, 256, 1, true> : CtShapeF256W {};
-template <>
-struct CtShapeSel<float, 256, -1, true> : CtShapeF256W {};
-#endif
-// (a build with an explicit -DSPFFT_CT256_E=... uses that one shape everywhere)
-#if defined(SPFFT_CT256_DEFAULT_SHAPE)
 template <>
 struct CtShapeSel<double, 256, 1, false> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
-#endif
 
 // Workgroup size cap of a shape: Sh::kMaxThr where a shape declares it (wide
 // 512-thread shapes), else kMaxThreads.
@@ -293,23 +232,10 @@ struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 // largest power of two <= b, at most 16 (line-fast lane mapping)
 __host__ __device__ constexpr int lf_lines(int b) {
   int p = 1;
-  while (p * 2 <= b && p * 2 <= SPFFT_LF_MAX_LINES) p *= 2;
+  while (p * 2 <= b && p * 2 <= kLfMaxLines) p *= 2;
   return p;
 }
 
-#ifndef SPFFT_PROBE_NO_COMPUTE
-#define SPFFT_PROBE_NO_COMPUTE 0
-#endif
-#ifndef SPFFT_PROBE_NO_EXCHANGE
-#define SPFFT_PROBE_NO_EXCHANGE 0
-#endif
-#ifndef SPFFT_LF_STRIDE
-#define SPFFT_LF_STRIDE 1
-#endif
-// FftCT: fetch a pass's twiddles before the LDS exchange that precedes it
-#ifndef SPFFT_TW_PREFETCH
-#define SPFFT_TW_PREFETCH 1
-#endif
 // Line stride of the line-fast mapping (lane = line b fastest, then position t).
 // gfx950 LDS banking (MI355X_MICROARCH.md §LDS): every ds_write and ds_read2 is
 // serviced in 16-lane groups on 32 banks (128 B), ds_read_b128 in four
@@ -352,7 +278,7 @@ struct FftCT {
   static constexpr int B0 =
       lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), Sh::kBudget, kMaxThr);
   static constexpr int B = LF ? lf_lines(B0) : B0;
-  static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B, PS) : LS0;
+  static constexpr int LS = LF ? lf_padded_stride<T>(N, B, PS) : LS0;
   static constexpr int NT = B * TP;
   static constexpr int RL = Sh::R2 > 1 ? Sh::R2 : (Sh::R1 > 1 ? Sh::R1 : Sh::R0);
 
@@ -368,9 +294,6 @@ struct FftCT {
 
   template <int R, int NS>
   __device__ static void compute(cx<T> (&v)[E], int t, const cx<TwT>* __restrict__ tw) {
-#if SPFFT_PROBE_NO_COMPUTE
-    return;  // timing probe only: results are wrong
-#endif
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {
       if (NS > 1) {
@@ -387,9 +310,6 @@ struct FftCT {
   // write pass outputs (Stockham positions) to LDS and read the next pass inputs
   template <int R, int NS, int RN>
   __device__ static void exchange(cx<T> (&v)[E], cx<T>* line, int t) {
-#if SPFFT_PROBE_NO_EXCHANGE
-    return;  // timing probe only: results are wrong
-#endif
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {
@@ -412,7 +332,7 @@ struct FftCT {
   // are issued before the LDS exchange that precedes the pass, so the table
   // read (an L1/L2 hit) overlaps the exchange instead of following it.
   // (not for the 32-element shapes of N = 1024: their registers are full)
-  static constexpr bool kTwPrefetch = SPFFT_TW_PREFETCH && TwPre && E <= 16;
+  static constexpr bool kTwPrefetch = TwPre && E <= 16;
   template <int R, int NS>
   struct PassTw {
     cx<TwT> w[(E / R) * (R - 1)];
@@ -621,7 +541,7 @@ struct FftMR {
   static constexpr int B0 =
       lines_per_block(TP, LS0 * static_cast<int>(sizeof(cx<T>)), kLdsBudget, kMaxThr);
   static constexpr int B = LF ? lf_lines(B0) : B0;
-  static constexpr int LS = (LF && SPFFT_LF_STRIDE) ? lf_padded_stride<T>(N, B, PS) : LS0;
+  static constexpr int LS = LF ? lf_padded_stride<T>(N, B, PS) : LS0;
   static constexpr int NT = B * TP;
 
   static constexpr int lines() { return B; }
@@ -775,13 +695,8 @@ struct RtPlan {
 // fewer passes per transform (240 = 16 * 15 instead of 16 * 5 * 3). Measured on
 // MI355X (profiles/README.md, session 12): +10-13% for fp64 at 100^3-240^3, but
 // -7% for fp32 at 240^3, where the larger pass switch costs more than the saved
-// pass. SPFFT_RT_PFA: -1 = per precision (fp64 on, fp32 off), 0 = off, 1 = on.
-#ifndef SPFFT_RT_PFA
-#define SPFFT_RT_PFA -1
-#endif
-__host__ __device__ constexpr bool rt_pfa(bool dbl) {
-  return SPFFT_RT_PFA < 0 ? dbl : SPFFT_RT_PFA != 0;
-}
+// pass: fp64 only.
+__host__ __device__ constexpr bool rt_pfa(bool dbl) { return dbl; }
 __host__ __device__ constexpr bool rt_composite_radix(int r) {
   return r == 6 || r == 10 || r == 12 || r == 15 || r == 20;
 }

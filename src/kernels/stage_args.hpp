@@ -141,20 +141,15 @@ int max_device_fft_length(bool doublePrecision);
 // 16..1024 (FftCT) and the mixed-radix lengths of SPFFT_MR_SIZES (FftMR).
 bool has_ct_kernel(int n);
 
-// Non-power-of-two lengths with compile-time mixed-radix kernels (X-macro).
-#ifndef SPFFT_MR
-#define SPFFT_MR 1
-#endif
+// Non-power-of-two lengths with compile-time mixed-radix kernels (X-macro;
+// user configuration: a build may list other lengths, or none, with
+// -DSPFFT_MR_SIZES(X)=..., trading compile time for run-time engines).
 #ifndef SPFFT_MR_SIZES
-#if SPFFT_MR
 #define SPFFT_MR_SIZES(X)                                                                 \
   X(48) X(60) X(72) X(80) X(90) X(96) X(100) X(108) X(120) X(125) X(135) X(144) X(150) X(160) \
   X(180) X(192) X(200) X(216) \
   X(240) X(288) X(320) X(360) X(384) \
   X(400) X(480)
-#else
-#define SPFFT_MR_SIZES(X)
-#endif
 #endif
 
 }  // namespace dev

@@ -14,97 +14,49 @@
 namespace spfft {
 namespace dev {
 
-#ifndef SPFFT_ROW_STAGE
-#define SPFFT_ROW_STAGE 1
-#endif
-
-#ifndef SPFFT_NT
-#define SPFFT_NT 1
-#endif
-#ifndef SPFFT_NT_VALUES
-#define SPFFT_NT_VALUES 0
-#endif
-
 // Streaming global accesses: every stage reads and writes each element once, so
 // loads and stores carry the non-temporal hint (measured on MI355X: 268 MB copy
 // 6.15-6.28 TB/s with nt vs 5.65-5.88 TB/s without, tools/probes/hbm_copy.hip).
 template <typename T>
 __device__ __forceinline__ cx<T> ld_stream(const cx<T>* p) {
-#if SPFFT_NT
   using V = T __attribute__((ext_vector_type(2)));
   const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
   return mk<T>(v.x, v.y);
-#else
-  return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
-#if SPFFT_NT
   using V = T __attribute__((ext_vector_type(2)));
   V w;
   w.x = v.x;
   w.y = v.y;
   __builtin_nontemporal_store(w, reinterpret_cast<V*>(p));
-#else
-  *p = v;
-#endif
 }
-// The [z][column][y] intermediate: streamed like the rest by default; with
-// SPFFT_NT_INTER=0 it keeps the default cache policy (plane-chunked ring mode,
-// where the x stage re-reads a chunk while it is resident in the Infinity Cache).
-#ifndef SPFFT_NT_INTER
-#define SPFFT_NT_INTER SPFFT_NT
-#endif
+// The [z][column][y] intermediate is streamed like the rest.
 template <typename T>
 __device__ __forceinline__ cx<T> ld_inter(const cx<T>* p) {
-#if SPFFT_NT_INTER
   return ld_stream(p);
-#else
-  return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void st_inter(cx<T>* p, cx<T> v) {
-#if SPFFT_NT_INTER
   st_stream(p, v);
-#else
-  *p = v;
-#endif
 }
 // Sparse frequency values: a stick's values rarely start on a cache-line
 // boundary, so neighbouring workgroups share lines; plain accesses keep them.
 template <typename T>
 __device__ __forceinline__ cx<T> ld_values(const cx<T>* p) {
-#if SPFFT_NT_VALUES
-  return ld_stream(p);
-#else
   return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void st_values(cx<T>* p, cx<T> v) {
-#if SPFFT_NT_VALUES
-  st_stream(p, v);
-#else
   *p = v;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ T ld_stream_real(const T* p) {
-#if SPFFT_NT
   return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void st_stream_real(T* p, T v) {
-#if SPFFT_NT
   __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
 }
 
 // Loads issued per lane before the first dependent LDS store: keeps U global
@@ -159,9 +111,6 @@ __device__ __forceinline__ void scatter_from_lds(const cx<T>* lds, int total, Sr
 // A full tile of a compile-time engine (every line present) copies with a
 // fully unrolled loop of compile-time trip count E: its LDS reads issue back to
 // back instead of one read, wait and store per iteration.
-#ifndef SPFFT_STATIC_COPY
-#define SPFFT_STATIC_COPY 1
-#endif
 template <class Eng, typename T, class Src, class St>
 __device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, St st) {
   if constexpr (Eng::kBatchedCopy) {
@@ -170,7 +119,7 @@ __device__ __forceinline__ void copy_out(const cx<T>* lds, int total, Src src, S
     using F = typename Eng::F;
     // (mixed-radix shapes can leave lanes idle: their tiles need not split evenly)
     constexpr bool kEven = (F::B * Eng::kN) % F::NT == 0;
-    if (SPFFT_STATIC_COPY && kEven && total == F::B * Eng::kN) {
+    if (kEven && total == F::B * Eng::kN) {
       constexpr int kIters = kEven ? F::B * Eng::kN / F::NT : 1;
       cx<T> v[kIters];
 #pragma unroll
@@ -759,10 +708,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
 }
 
-#ifndef SPFFT_ZB_REGDESC
-#define SPFFT_ZB_REGDESC 1
-#endif
-
 // z stage for "simple" sticks (values of a stick contiguous, <= 2 z-runs; the
 // common stick-major input): every lane maps its FFT positions z straight to
 // value offsets, so values are loaded into registers and written back with
@@ -815,7 +760,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     hermitian_lines(eng, lds, a.zeroStick - s0, 1, n);
     eng.lds_to_global(lds, tw, store);
   } else {
-#if SPFFT_ZB_REGDESC
     // compile-time engines load only the lane's own line (b == lane_line(),
     // the FftCT/FftMR contract): its descriptor is read from LDS once into
     // registers and the value offset is a branch-free select. Reading d[b] in
@@ -834,9 +778,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
       return (in0 || in1) ? ld_values(&vals[j]) : czero<T>();
     }, store);
-#else
-    eng.global_to_global(lds, tw, load, store);
-#endif
   }
   release_remote(a.remote);
 }
@@ -893,26 +834,21 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
 }
 
-// y-stage tile order. SPFFT_Y_ZFAST=1: plane blocks fastest in the grid, so
-// the workgroups in flight cover a few whole columns: each stick is read (or
-// written) entirely while it is open in the DRAM row buffers, and the
-// [z][column][y] rows of a plane are written as one contiguous run.
-#ifndef SPFFT_Y_ZFAST
-#define SPFFT_Y_ZFAST 1
-#endif
+// y-stage tile order: plane blocks fastest in the grid, so the workgroups in
+// flight cover a few whole columns: each stick is read (or written) entirely
+// while it is open in the DRAM row buffers, and the [z][column][y] rows of a
+// plane are written as one contiguous run.
 __device__ __forceinline__ int y_tile_col() {
   int bx, by;
   block_tile(bx, by);
-  return SPFFT_Y_ZFAST ? by : bx;
+  return by;
 }
 __device__ __forceinline__ int y_tile_zblock() {
   int bx, by;
   block_tile(bx, by);
-  return SPFFT_Y_ZFAST ? bx : by;
+  return bx;
 }
-inline dim3 y_grid(int cols, int zblocks, unsigned batch = 1) {
-  return SPFFT_Y_ZFAST ? dim3(zblocks, cols, batch) : dim3(cols, zblocks, batch);
-}
+inline dim3 y_grid(int cols, int zblocks, unsigned batch = 1) { return dim3(zblocks, cols, batch); }
 
 // ---------------------------------------------------------------- y stage
 // Whether the column with run descriptor d has a stick entry at y, and its base
@@ -939,12 +875,6 @@ __device__ __forceinline__ bool col_desc_find(const ColDesc& d, long long stride
 // Every kernel keeps a single FFT call site whichever source is used: the
 // run-time engines inline their whole pass switch per call site, and a second
 // copy doubled their register demand (profiles/r2_s1/rt_regression.txt).
-#ifndef SPFFT_Y_TABLE
-#define SPFFT_Y_TABLE 1
-#endif
-#ifndef SPFFT_YF_TABLE
-#define SPFFT_YF_TABLE 1
-#endif
 // engines whose store positions can be enumerated ahead of run() (FftCT)
 template <class Eng, class = void>
 struct has_store_pos : std::false_type {};
@@ -1064,7 +994,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
   const bool x0 = c == a.colOfX0;
-  constexpr bool kTable = y_table<Eng, SPFFT_Y_TABLE>();
+  constexpr bool kTable = y_table<Eng, true>();
   const ColEntries<Eng> ce(eng, a, lds, c, !x0, kTable && !x0);
   const BT* zsrc = reinterpret_cast<const BT*>(gZeroSource);
   auto load = [&](int b, int pos) -> cx<T> {
@@ -1131,7 +1061,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int c = a.colBegin + y_tile_col();
   const int z0 = a.zBegin + y_tile_zblock() * B;
   const int zl = min(B, a.L - z0);
-  constexpr bool kTable = y_table<Eng, SPFFT_YF_TABLE && has_store_pos<Eng>::value>();
+  constexpr bool kTable = y_table<Eng, has_store_pos<Eng>::value>();
   const ColEntries<Eng> ce(eng, a, lds, c, true, kTable);
   auto load = [&](int b, int pos) -> cx<T> {
     if (b >= zl) return czero<T>();
@@ -1157,12 +1087,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
     long long base;
     if (ce.find(pos, base) && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
   };
-#if SPFFT_ROW_STAGE
   stage_rows(eng, lds, zl, n, load);
   eng.lds_to_global(lds, tw, store);
-#else
-  eng.global_to_global(lds, tw, load, store);
-#endif
   release_remote(a.remote);
 }
 
@@ -1185,10 +1111,8 @@ __device__ __forceinline__ int xcol_of(const XArgs& a, const int* xCol, int x) {
 
 // Packed-real C2R with the pre-pass folded into the first FFT pass's loads
 // (compile-time engines): 66.9 -> 54.8 us at 256^3 fp64, R2C bench +2% fp64,
-// +3% fp32 (profiles/r2_s1/shape_ab.txt). 0 restores the LDS-staged pre-pass.
-#ifndef SPFFT_C2R_DIRECT
-#define SPFFT_C2R_DIRECT 1
-#endif
+// +3% fp32 (profiles/r2_s1/shape_ab.txt); the run-time engines stage the
+// pre-pass in LDS.
 
 // ---------------------------------------------------------------- x stage
 // Backward x stage with the line-fast engine: lane (line = row y, pos = x)
@@ -1271,12 +1195,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const int c = dense ? (pos < nFreq ? pos : -1) : xCol[pos];
     if (c >= 0 && b < yl) st_inter(&dst[c * rowStride + b], v);
   };
-#if SPFFT_ROW_STAGE
   stage_rows(eng, lds, yl, n, load);
   eng.lds_to_global(lds, tw, store);
-#else
-  eng.global_to_global(lds, tw, load, store);
-#endif
 }
 
 // Packed-real x stage (R2C transforms with even dimX): a real row of length n
@@ -1307,7 +1227,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
   build_xcol(a, xCol, h + 1);
   const cx<T>* src = inter + static_cast<long long>(zl) * a.interZStride + y0;
   const int yl = min(B, a.Y - y0);
-#if SPFFT_C2R_DIRECT
   if constexpr (!Eng::kBatchedCopy) {
     // pre-pass folded into the FFT's first-pass loads: the lane that needs Z[k]
     // loads X[k] and X[h-k] itself (the mirror column is the same workgroup's
@@ -1336,7 +1255,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     }, [&](int idx, cx<T> v) { st_stream(&out[idx], v); });
     return;
   }
-#endif
   // columns X[0..h] of the block's rows, each element loaded once (lanes run
   // over rows: contiguous column segments)
   gather_to_lds(lds, h * B, [&](int idx) -> cx<T> {
@@ -1397,7 +1315,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return b >= yl ? czero<T>() : ld_stream(row0 + static_cast<long long>(b) * h + m);
   };
   if constexpr (!Eng::kBatchedCopy && !Eng::kLineFast) {
-    // row-mapped engine (SPFFT_R2C_ROWMAP): a line's lanes are adjacent, so the
+    // row-mapped engine (x_stage_fwd.hip): a line's lanes are adjacent, so the
     // first pass loads the real rows straight from global memory
     eng.global_to_lds(lds, twh, rowLoad);
   } else {

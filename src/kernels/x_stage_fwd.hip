@@ -1,12 +1,8 @@
 // x-stage forward launcher: space domain rows -> [z][column][y] (C2C, R2C);
 // its own translation unit so the x-stage kernels compile in parallel.
-// Engine lane mapping of the packed-real R2C x stage: 1 = row-mapped (the
-// first FFT pass loads the real rows directly), 0 = line-fast with the rows
-// staged through LDS. Measured at 256^3 (profiles/r2_s1/shape_ab.txt): 58.9 ->
-// 56.8 us with the radix-8 row-mapped shape.
-#ifndef SPFFT_R2C_ROWMAP
-#define SPFFT_R2C_ROWMAP 1
-#endif
+// The packed-real R2C x stage runs the row-mapped engine (the first FFT pass
+// loads the real rows directly) rather than the line-fast one with the rows
+// staged through LDS: 58.9 -> 56.8 us at 256^3 (profiles/r2_s1/shape_ab.txt).
 #include "kernels/stage_kernels.hpp"
 
 namespace spfft {
@@ -17,7 +13,7 @@ void launch_x_forward(const XArgs& a, bool r2c, const void* space, cx<T>* inter,
                       const cx<T>* tw, const cx<T>* twHalf, hipStream_t stream) {
   if (a.L <= a.zBegin || a.Y <= 0) return;
   if (r2c && twHalf && a.n % 2 == 0 && a.n >= 4) {
-    with_engine<T, -1, !SPFFT_R2C_ROWMAP>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
+    with_engine<T, -1, false>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
       auto k = x_forward_r2c_kernel<decltype(eng), T>;
       const std::size_t ldsTotal = lds + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
       prepare_kernel(k, ldsTotal);

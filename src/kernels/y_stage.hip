@@ -10,7 +10,7 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
   if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
   with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = y_backward_kernel<decltype(eng), T, BT>;
-    const std::size_t ldsTotal = lds + col_entries_lds(a, true, y_table<decltype(eng), SPFFT_Y_TABLE>());
+    const std::size_t ldsTotal = lds + col_entries_lds(a, true, y_table<decltype(eng), true>());
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines), batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        in, inter, tw);

@@ -11,7 +11,7 @@ void launch_y_forward(const YArgs& a, const cx<T>* inter, BT* out, const cx<T>* 
   if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
   with_engine<T, -1, true, !std::is_same<T, float>::value>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     auto k = y_forward_kernel<decltype(eng), T, BT>;
-    const std::size_t ldsTotal = lds + col_entries_lds(a, false, y_table<decltype(eng), SPFFT_YF_TABLE && has_store_pos<decltype(eng)>::value>());
+    const std::size_t ldsTotal = lds + col_entries_lds(a, false, y_table<decltype(eng), has_store_pos<decltype(eng)>::value>());
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines), batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
                        inter, out, tw);

@@ -158,6 +158,86 @@ public:
     return std::unique_ptr<ExchangeRequest>(r.release());
   }
 
+  // MPI_Alltoallw with one hvector datatype per peer (count blocks of a
+  // contiguous unit type, byte strides): MPI gathers and scatters the strided
+  // blocks itself, no pack buffer (reference UNBUFFERED,
+  // src/transpose/transpose_mpi_unbuffered_host.cpp:66-181).
+  struct WTypes {
+    std::vector<MPI_Datatype> st, rt;
+    std::vector<int> sc, sd, rc, rd;
+    ~WTypes() {
+      if (mpi_finalized()) return;
+      for (auto* v : {&st, &rt})
+        for (MPI_Datatype& t : *v)
+          if (t != MPI_DATATYPE_NULL && t != MPI_BYTE) MPI_Type_free(&t);
+    }
+  };
+  static MPI_Datatype strided_type(const StridedLayout& l) {
+    std::size_t unit = 1;
+    for (std::size_t u : {std::size_t(16), std::size_t(8), std::size_t(4)})
+      if (l.blockBytes % u == 0) {
+        unit = u;
+        break;
+      }
+    if (l.count > static_cast<std::size_t>(INT_MAX) || l.blockBytes / unit > static_cast<std::size_t>(INT_MAX))
+      throw OverflowError();
+    MPI_Datatype base = MPI_DATATYPE_NULL, t = MPI_DATATYPE_NULL;
+    mpi_check(MPI_Type_contiguous(static_cast<int>(unit), MPI_BYTE, &base));
+    mpi_check(MPI_Type_create_hvector(static_cast<int>(l.count), static_cast<int>(l.blockBytes / unit),
+                                      static_cast<MPI_Aint>(l.strideBytes), base, &t));
+    mpi_check(MPI_Type_free(&base));
+    mpi_check(MPI_Type_commit(&t));
+    return t;
+  }
+  void make_wtypes(WTypes& w, const StridedLayout* sl, const StridedLayout* rl) const {
+    w.st.assign(size_, MPI_BYTE);
+    w.rt.assign(size_, MPI_BYTE);
+    w.sc.assign(size_, 0);
+    w.sd.assign(size_, 0);
+    w.rc.assign(size_, 0);
+    w.rd.assign(size_, 0);
+    for (int r = 0; r < size_; ++r) {
+      if (sl[r].offset > static_cast<std::size_t>(INT_MAX) || rl[r].offset > static_cast<std::size_t>(INT_MAX))
+        throw OverflowError();
+      if (sl[r].count > 0 && sl[r].blockBytes > 0) {
+        w.st[r] = strided_type(sl[r]);
+        w.sc[r] = 1;
+        w.sd[r] = static_cast<int>(sl[r].offset);
+      }
+      if (rl[r].count > 0 && rl[r].blockBytes > 0) {
+        w.rt[r] = strided_type(rl[r]);
+        w.rc[r] = 1;
+        w.rd[r] = static_cast<int>(rl[r].offset);
+      }
+    }
+  }
+  void alltoallw(const void* send, const StridedLayout* sl, void* recv,
+                 const StridedLayout* rl) override {
+    WTypes w;
+    make_wtypes(w, sl, rl);
+    mpi_check(MPI_Alltoallw(send, w.sc.data(), w.sd.data(), w.st.data(), recv, w.rc.data(), w.rd.data(),
+                            w.rt.data(), comm_));
+  }
+  struct WRequest : ExchangeRequest {
+    WTypes types;
+    MPI_Request req = MPI_REQUEST_NULL;
+    ~WRequest() override {
+      if (req != MPI_REQUEST_NULL && !mpi_finalized()) MPI_Wait(&req, MPI_STATUS_IGNORE);
+    }
+    void wait() override {
+      if (req != MPI_REQUEST_NULL) mpi_check(MPI_Wait(&req, MPI_STATUS_IGNORE));
+    }
+  };
+  std::unique_ptr<ExchangeRequest> ialltoallw(const void* send, const StridedLayout* sl, void* recv,
+                                              const StridedLayout* rl) override {
+    std::unique_ptr<WRequest> r(new WRequest());
+    make_wtypes(r->types, sl, rl);
+    WTypes& w = r->types;
+    mpi_check(MPI_Ialltoallw(send, w.sc.data(), w.sd.data(), w.st.data(), recv, w.rc.data(), w.rd.data(),
+                             w.rt.data(), comm_, &r->req));
+    return std::unique_ptr<ExchangeRequest>(r.release());
+  }
+
   void barrier() override { mpi_check(MPI_Barrier(comm_)); }
 
   std::shared_ptr<Communicator> duplicate() const override {

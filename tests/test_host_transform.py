@@ -87,10 +87,13 @@ def test_single_precision_host():
     assert max_rel_error(out, dense_backward(idx, vals, dims)) < 1e-5
 
 
-@pytest.mark.parametrize("dims", [(67, 3, 2), (101, 103, 4), (127, 2, 131), (2, 257, 3), (199, 1, 1)])
+@pytest.mark.parametrize("dims", [(67, 3, 2), (101, 103, 4), (127, 2, 131), (2, 257, 3), (199, 1, 1),
+                                  (202, 3, 2), (3, 134, 5), (4, 3, 206)])
 @pytest.mark.parametrize("r2c", [False, True])
 def test_large_prime_bluestein(dims, r2c):
-    """Lengths with a prime factor > 61 run through Bluestein's algorithm (host)."""
+    """Lengths with a prime factor > 61 (host, batched): primes whose n - 1 has a
+    direct plan run Rader's algorithm (67, 101, 103, 127, 131, 199, 257), other
+    lengths (2 * 101, 2 * 67, 2 * 103) Bluestein's chirp-z convolution."""
     nx, ny, nz = dims
     rng = np.random.default_rng(3)
     idx = create_value_indices(rng, [1.0], 0.8, 0.9, nx, ny, nz, r2c)[0]
@@ -140,7 +143,7 @@ def test_batched_engine_paths(dims, ttype, fuse, single, monkeypatch):
     """The batched SIMD host engine: fused plane-block y/x path and separate
     stages (SPFFT_HOST_FUSE), packed-real (even dimX) and complex (odd dimX)
     C2R/R2C x lines, partial batches (plane / row / stick counts that are not a
-    multiple of the SIMD width), Bluestein lengths (67, 131) run line by line."""
+    multiple of the SIMD width), prime lengths (67, 131: Rader) on SIMD lanes too."""
     monkeypatch.setenv("SPFFT_HOST_FUSE", fuse)
     nx, ny, nz = dims
     r2c = ttype == "r2c"

@@ -120,3 +120,22 @@ def test_host_multi_transform_nonblocking_exchange_mpi(tmp_path):
     assert j["results"][0]["transforms_per_second"] > 0
     for name in ("backward_exchange_start", "forward_exchange_start", "exchange_wait"):
         assert name in text, name
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_host_unbuffered_alltoallw_mpi(tmp_path, nranks):
+    """Host UNBUFFERED under mpiexec: the z stage keeps whole sticks and the exchange
+    is one MPI_(I)alltoallw with hvector datatypes per peer (no pack or unpack pass;
+    reference: src/transpose/transpose_mpi_unbuffered_host.cpp:66-181). The bench's
+    timing tree shows the alltoallw scopes, non-blocking under multi_transform."""
+    import json
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = tmp_path / "unbuf.json"
+    _run([MPIEXEC, "-n", str(nranks), _prog("spfft_bench"), "-d", "30", "28", "26", "-r", "3",
+          "-m", "2", "-o", str(out), "-e", "unbuffered", "-p", "cpu", "--cutoff", "0.5"])
+    text = out.read_text()
+    j = json.loads(text)
+    assert j["results"][0]["transforms_per_second"] > 0
+    assert "alltoallw" in text
+    assert "pack" not in text

@@ -1,6 +1,8 @@
-"""Builds kernel-tuning variants of libspfft_amd.so (compile-time knobs) into
+"""Builds variants of libspfft_amd.so with extra compile flags into
 spfft_amd/_native/variants/libspfft_amd_<name>.so; select one at run time with
-SPFFT_AMD_LIBRARY=<path>.
+SPFFT_AMD_LIBRARY=<path>. The product kernels carry no A/B switches: an
+experiment is a source patch plus a variant build of it (e.g. a different
+SPFFT_MR_SIZES list, the one user-facing kernel configuration).
 
     python tools/build_variants.py name=-DKNOB=1,-DOTHER=2 [name2=...]
 """
