@@ -88,6 +88,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   colDescs_ = env_int("SPFFT_COL_DESC", 1, 0, 1) != 0;
   build_col_desc(colDesc_, cb, layout_.slabStride);
   upload(colX_, p.colX);
+  if (longX_) upload(xToCol_, p.xToCol);
   upload(twX_, make_twiddles<T>(p.dimX));
   // packed-real x stage for R2C with even dimX (SPFFT_R2C_PACKED=0 disables)
   if (!longX_ && p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4 &&
@@ -848,6 +849,7 @@ dev::XArgs GpuExecutor<T>::xargs() const {
   a.interStride = interStride_;
   a.interZStride = static_cast<long long>(p.num_columns()) * interStride_;
   a.colX = colX_ ? colX_->data<int>() : nullptr;
+  a.xToCol = xToCol_ ? xToCol_->data<int>() : nullptr;
   return a;
 }
 

@@ -155,7 +155,7 @@ private:
   std::vector<long long> segStride_;
   std::unique_ptr<DeviceBuffer> zTab_, zTabRemote_;
   void upload_ztab(std::unique_ptr<DeviceBuffer>& dst, const std::vector<long long>& segDispl);
-  std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_;
+  std::unique_ptr<DeviceBuffer> colOffsets_, colY_, colBase_, colX_, xToCol_;
   // per-column run descriptors of the y stage (YArgs::colDesc), one per colBase
   // table in use; null when some column needs more than kColRuns runs.
   // SPFFT_COL_DESC=0 disables them.

@@ -357,7 +357,7 @@ struct FftCT {
   }
 
   template <class Load>
-  __device__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<TwT>* __restrict__ tw,
+  __device__ __forceinline__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<TwT>* __restrict__ tw,
                                    Load load, int b, int t) {
     cx<T>* line = lds + b * LS;
 #pragma unroll
@@ -419,7 +419,7 @@ struct FftCT {
   }
 
   template <class Load, class Store>
-  __device__ static void run(cx<T>* lds, const cx<TwT>* __restrict__ tw, Load load, Store store) {
+  __device__ __forceinline__ static void run(cx<T>* lds, const cx<TwT>* __restrict__ tw, Load load, Store store) {
     const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
@@ -433,7 +433,7 @@ struct FftCT {
 
   // Result left in LDS at out_at(b, pos); ends with a barrier.
   template <class Load>
-  __device__ static void run_to_lds(cx<T>* lds, const cx<TwT>* __restrict__ tw, Load load) {
+  __device__ __forceinline__ static void run_to_lds(cx<T>* lds, const cx<TwT>* __restrict__ tw, Load load) {
     const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
@@ -626,7 +626,7 @@ struct FftMR {
   }
 
   template <class Load>
-  __device__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<T>* __restrict__ tw,
+  __device__ __forceinline__ static void transform(cx<T> (&v)[E], cx<T>* lds, const cx<T>* __restrict__ tw,
                                    Load load, int b, int t) {
     cx<T>* line = lds + b * LS;
     gather<0>(v, line, load, b, t);
@@ -637,7 +637,7 @@ struct FftMR {
   // Result delivered to store(b, pos, value), only for the lane's own line
   // (the FftCT contract); consecutive lanes -> consecutive positions.
   template <class Load, class Store>
-  __device__ static void run(cx<T>* lds, const cx<T>* __restrict__ tw, Load load, Store store) {
+  __device__ __forceinline__ static void run(cx<T>* lds, const cx<T>* __restrict__ tw, Load load, Store store) {
     const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
@@ -653,7 +653,7 @@ struct FftMR {
 
   // Result left in LDS at out_at(b, pos); ends with a barrier.
   template <class Load>
-  __device__ static void run_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Load load) {
+  __device__ __forceinline__ static void run_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Load load) {
     const int b = lane_line(), t = lane_pos();
     cx<T> v[E];
     transform(v, lds, tw, load, b, t);
@@ -858,7 +858,7 @@ struct FftRT {
 
   // Input in region 0 at in_at(b, pos); returns the region holding the result
   // (index b*ls + pos). Ends with a barrier.
-  __device__ static cx<T>* run_in_lds(const RtPlan& p, cx<T>* lds, const cx<T>* __restrict__ tw) {
+  __device__ __forceinline__ static cx<T>* run_in_lds(const RtPlan& p, cx<T>* lds, const cx<T>* __restrict__ tw) {
     if (p.inplace) {
       run_inplace(p, lds, tw);
       return lds;
@@ -867,7 +867,7 @@ struct FftRT {
   }
 
   // Ping-pong between two LDS regions (input in src); returns the result region.
-  __device__ static cx<T>* run_between(const RtPlan& p, cx<T>* src, cx<T>* dst,
+  __device__ __forceinline__ static cx<T>* run_between(const RtPlan& p, cx<T>* src, cx<T>* dst,
                                        const cx<T>* __restrict__ tw) {
     int ns = 1;
     for (int i = 0; i < p.np; ++i) {

@@ -57,49 +57,245 @@ __global__ void __launch_bounds__(256) herm_lines_kernel(cx<T>* base, long long 
 // ------------------------------------------------------------ four-step
 struct PassArgs {
   int n1, n2;
-  long long srcStride, dstStride;
+  long long stride;  // work buffer line stride
   int blocksPerLine;
+  int fence;  // rows pass: release its stores system-wide at exit (peer-write exchange)
 };
 
-// columns pass, in place: for every column j2 of a line viewed as [n1][n2]:
-// FFT_n1 over j1 -> k1, times exp(S 2 pi i j2 k1 / (n1 n2)). Lanes walk
-// consecutive columns (coalesced rows of the [n1][n2] view).
-template <class Eng, typename T, int S>
-__global__ void __launch_bounds__(Eng::kBlock)
-    long_cols_kernel(Eng eng, PassArgs a, cx<T>* data, const cx<T>* __restrict__ tw1,
-                     const cx<T>* __restrict__ twM) {
+// Value at position z of a line after the reference's two-pass hermitian
+// completion (src/symmetry/symmetry_host.hpp:68-94: only zero entries are
+// filled), computed pointwise from the original entries: the (0,0) stick and
+// the x = 0 column of R2C transforms, inside the fused loads.
+template <typename T, class Get>
+__device__ __forceinline__ cx<T> hermitian_at(Get get, int z, int n) {
+  if (z == 0) return get(0);
+  const cx<T> v = get(z);
+  if (2 * z <= n) return nonzero(v) ? v : conj(get(n - z));
+  const cx<T> u = get(n - z);
+  return nonzero(u) ? conj(u) : v;
+}
+
+// Sources and sinks of the four-step passes. The columns pass reads its
+// elements through io.load(line, pos), the rows pass delivers its results to
+// io.store(line, pos, v): the stage launchers configure value gathers, the
+// exchange layouts, hermitian fills and the x -> column tables there, so no
+// glue kernel runs before the columns pass or after the rows pass. The variant
+// is a run-time field (a workgroup-uniform branch per element): one kernel per
+// engine, precision and exchange type, not one per call site.
+template <typename T, typename BT>
+struct LongIO {
+  enum Kind : int {
+    kPlain,      // src[line * srcStride + pos] / dst[line * dstStride + pos]
+    kFilter,     // store: dst[...] = v * filt[pos] (Bluestein convolution)
+    kZValues,    // load / store: the sparse values of stick s0 + line (simple sticks)
+    kZSeg,       // load / store: the exchange layout (seg_index)
+    kYCols,      // load / store: the stick entries of column c through its run descriptor
+    kXCols,      // load: X[x] of row `line` from the intermediate's columns (x -> column table)
+    kXPacked,    // load: packed-real C2R pre-pass of X[k], X[h-k]
+    kXOdd,       // load: hermitian-extended complex row (odd length C2R)
+    kXReal,      // load: real row as complex
+    kXPut,       // store: the columns that hold sticks
+    kReal,       // store: real part
+  };
+  int lk = kPlain, sk = kPlain;
+  int n = 0;  // line length
+  const cx<T>* src = nullptr;
+  long long srcStride = 0;
+  cx<T>* dst = nullptr;
+  long long dstStride = 0;
+  // Bluestein: chirp on the load (pos < chirpN: x d_pos, else 0) or on the store
+  // (pos < chirpN: d_pos v * outScale, else dropped); d = conj(chirp) when chirpConj
+  const cx<T>* chirpIn = nullptr;
+  const cx<T>* chirpOut = nullptr;
+  int chirpN = 0, chirpConj = 0;
+  T outScale = T(1);
+  const cx<T>* filt = nullptr;
+  // z stage: exchange-side addressing of ZArgs (single, stickStride, zTab)
+  int zSingle = 1;
+  long long zStride = 0;
+  const long long* zTab = nullptr;
+  const StickDesc* desc = nullptr;
+  const cx<T>* values = nullptr;
+  cx<T>* valuesOut = nullptr;
+  const BT* xin = nullptr;
+  BT* xout = nullptr;
+  int s0 = 0, zeroStick = -1;
+  T vscale = T(1);
+  // y stage
+  const ColDesc* colDesc = nullptr;
+  long long colStride = 0;
+  int zb = 0, C = 1, x0 = -1;
+  // x stage
+  const cx<T>* inter = nullptr;
+  cx<T>* interOut = nullptr;
+  long long iz = 0, is = 0;
+  int Y = 1, nf = 0, X = 0, h = 0;
+  const int* xToCol = nullptr;
+  const cx<T>* twFull = nullptr;
+  const T* realSrc = nullptr;
+  T* realDst = nullptr;
+
+  __device__ __forceinline__ long long seg(long long line, int pos) const {
+    const long long s = s0 + line;
+    if (zSingle == 1) return s * zStride + pos;
+    using V = long long __attribute__((ext_vector_type(2)));
+    const V t = *reinterpret_cast<const V*>(zTab + 2 * pos);
+    return t.x + s * t.y;
+  }
+  __device__ __forceinline__ cx<T> zvalue(long long s, int z) const {
+    const StickDesc& q = desc[s0 + s];
+    auto get = [&](int zz) -> cx<T> {
+      const int j = desc_offset(q, zz);
+      return j < 0 ? czero<T>() : values[q.valueStart + j];
+    };
+    return s0 + s == zeroStick ? hermitian_at<T>(get, z, n) : get(z);
+  }
+  __device__ __forceinline__ cx<T> ycol(long long l, int y) const {
+    const int zz = static_cast<int>(l / C), c = static_cast<int>(l - static_cast<long long>(zz) * C);
+    const ColDesc& d = colDesc[c];
+    auto get = [&](int yy) -> cx<T> {
+      long long base;
+      return col_desc_find(d, colStride, yy, base) ? cvt<T>(xin[base + zb + zz]) : czero<T>();
+    };
+    return c == x0 ? hermitian_at<T>(get, y, n) : get(y);
+  }
+  __device__ __forceinline__ cx<T> xcol(long long l, int x) const {
+    const long long zz = l / Y, y = l - zz * Y;
+    const int c = x < nf ? xToCol[x] : -1;
+    return c < 0 ? czero<T>() : inter[zz * iz + c * is + y];
+  }
+  __device__ __forceinline__ cx<T> base_load(long long line, int pos) const {
+    switch (lk) {
+      case kZValues:
+        return zvalue(line, pos);
+      case kZSeg:
+        return cvt<T>(xin[seg(line, pos)]);
+      case kYCols:
+        return ycol(line, pos);
+      case kXCols:
+        return xcol(line, pos);
+      case kXPacked: {
+        cx<T> xk = xcol(line, pos), xm = xcol(line, h - pos);
+        if (pos == 0) {
+          xk.y = T(0);
+          xm.y = T(0);
+        }
+        const cx<T> xmc = conj(xm);
+        return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twFull[pos]));
+      }
+      case kXOdd:
+        return pos < nf ? xcol(line, pos) : conj(xcol(line, X - pos));
+      case kXReal:
+        return mk<T>(realSrc[line * X + pos], T(0));
+      default:
+        return src[line * srcStride + pos];
+    }
+  }
+  __device__ __forceinline__ cx<T> load(long long line, int pos) const {
+    if (chirpIn) {
+      if (pos >= chirpN) return czero<T>();
+      const cx<T> d = chirpConj ? conj(chirpIn[pos]) : chirpIn[pos];
+      return cmul(base_load(line, pos), d);
+    }
+    return base_load(line, pos);
+  }
+  __device__ __forceinline__ void store(long long line, int pos, cx<T> v) const {
+    if (chirpOut) {
+      if (pos >= chirpN) return;
+      const cx<T> d = chirpConj ? conj(chirpOut[pos]) : chirpOut[pos];
+      v = scale(cmul(v, d), outScale);
+    }
+    switch (sk) {
+      case kFilter:
+        dst[line * dstStride + pos] = cmul(v, filt[pos]);
+        return;
+      case kZSeg:
+        xout[seg(line, pos)] = cvt<typename BT::value_type>(v);
+        return;
+      case kZValues: {
+        const StickDesc& q = desc[s0 + line];
+        const int j = desc_offset(q, pos);
+        if (j >= 0) valuesOut[q.valueStart + j] = scale(v, vscale);
+        return;
+      }
+      case kYCols: {
+        const int zz = static_cast<int>(line / C), c = static_cast<int>(line - static_cast<long long>(zz) * C);
+        long long base;
+        if (col_desc_find(colDesc[c], colStride, pos, base)) xout[base + zb + zz] = cvt<typename BT::value_type>(v);
+        return;
+      }
+      case kXPut: {
+        const int c = pos < nf ? xToCol[pos] : -1;
+        if (c < 0) return;
+        const long long zz = line / Y, y = line - zz * Y;
+        interOut[zz * iz + c * is + y] = v;
+        return;
+      }
+      case kReal:
+        realDst[line * X + pos] = v.x;
+        return;
+      default:
+        dst[line * dstStride + pos] = v;
+    }
+  }
+};
+
+// columns pass: for every column j2 of a line viewed as [n1][n2]: FFT_n1 over
+// j1 -> k1, times exp(S 2 pi i j2 k1 / (n1 n2)), into work (same positions).
+// The line comes from io.load(line, j1 n2 + j2) (fused) or from work itself
+// (plain: the run-time engines, whose pass switch leaves no registers for the
+// IO variants, read a line a glue pass staged). Lanes walk consecutive columns
+// (coalesced rows of the [n1][n2] view).
+template <class Eng, typename T, class Src>
+__device__ __forceinline__ void long_cols_body(const Eng& eng, const PassArgs& a, Src src, cx<T>* work,
+                                               const cx<T>* __restrict__ tw1, const cx<T>* __restrict__ twM,
+                                               int S) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const long long line = blockIdx.x / a.blocksPerLine;
   const int j20 = static_cast<int>(blockIdx.x % a.blocksPerLine) * B;
-  cx<T>* base = data + line * a.srcStride;
+  cx<T>* base = work + line * a.stride;
   const int total = B * a.n1;
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
     const int b = idx % B, j1 = idx / B, j2 = j20 + b;
-    lds[eng.in_at(b, j1)] = j2 < a.n2 ? base[static_cast<long long>(j1) * a.n2 + j2] : czero<T>();
+    lds[eng.in_at(b, j1)] = j2 < a.n2 ? src(line, j1 * a.n2 + j2) : czero<T>();
   }
   __syncthreads();
   eng.lds_to_lds(lds, tw1);
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
     const int b = idx % B, k1 = idx / B, j2 = j20 + b;
-    if (j2 < a.n2)
-      base[static_cast<long long>(k1) * a.n2 + j2] =
-          twm<S>(lds[eng.out_at(b, k1)], twM[static_cast<long long>(j2) * k1]);
+    if (j2 < a.n2) {
+      const cx<T> w = twM[static_cast<long long>(j2) * k1];
+      const cx<T> v = lds[eng.out_at(b, k1)];
+      base[static_cast<long long>(k1) * a.n2 + j2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
+    }
   }
 }
-
-// rows pass, out of place: for every row k1: FFT_n2 over j2 -> k2, stored at
-// the natural position k1 + n1 k2 (loads walk rows, stores walk rows fastest)
+template <class Eng, typename T, typename BT, int S>
+__global__ void __launch_bounds__(Eng::kBlock)
+    long_cols_kernel(Eng eng, PassArgs a, LongIO<T, BT> io, cx<T>* work, const cx<T>* __restrict__ tw1,
+                     const cx<T>* __restrict__ twM) {
+  long_cols_body<Eng, T>(eng, a, [&](long long l, int p) { return io.load(l, p); }, work, tw1, twM, S);
+}
 template <class Eng, typename T, int S>
 __global__ void __launch_bounds__(Eng::kBlock)
-    long_rows_kernel(Eng eng, PassArgs a, const cx<T>* src, cx<T>* dst,
-                     const cx<T>* __restrict__ tw2) {
+    long_cols_plain_kernel(Eng eng, PassArgs a, cx<T>* work, const cx<T>* __restrict__ tw1,
+                           const cx<T>* __restrict__ twM) {
+  long_cols_body<Eng, T>(eng, a, [&](long long l, int p) { return work[l * a.stride + p]; }, work, tw1,
+                         twM, S);
+}
+
+// rows pass: for every row k1 of work: FFT_n2 over j2 -> k2, delivered to
+// position k1 + n1 k2 of io.store (fused) or of out (plain, natural order,
+// stride n1 n2, for a glue pass); loads walk rows, stores walk k1 fastest
+template <class Eng, typename T, class Dst>
+__device__ __forceinline__ void long_rows_body(const Eng& eng, const PassArgs& a, const cx<T>* work,
+                                               Dst dst, const cx<T>* __restrict__ tw2) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
   const long long line = blockIdx.x / a.blocksPerLine;
   const int k10 = static_cast<int>(blockIdx.x % a.blocksPerLine) * B;
-  const cx<T>* s = src + line * a.srcStride;
-  cx<T>* d = dst + line * a.dstStride;
+  const cx<T>* s = work + line * a.stride;
   const int total = B * a.n2;
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
     const int b = idx / a.n2, j2 = idx - b * a.n2, k1 = k10 + b;
@@ -109,72 +305,146 @@ __global__ void __launch_bounds__(Eng::kBlock)
   eng.lds_to_lds(lds, tw2);
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
     const int b = idx % B, k2 = idx / B, k1 = k10 + b;
-    if (k1 < a.n1) d[k1 + static_cast<long long>(a.n1) * k2] = lds[eng.out_at(b, k2)];
+    if (k1 < a.n1) dst(line, k1 + a.n1 * k2, lds[eng.out_at(b, k2)]);
+  }
+  release_remote(a.fence);
+}
+template <class Eng, typename T, typename BT, int S>
+__global__ void __launch_bounds__(Eng::kBlock)
+    long_rows_kernel(Eng eng, PassArgs a, const cx<T>* work, LongIO<T, BT> io,
+                     const cx<T>* __restrict__ tw2) {
+  long_rows_body<Eng, T>(eng, a, work, [&](long long l, int p, cx<T> v) { io.store(l, p, v); }, tw2);
+}
+template <class Eng, typename T, int S>
+__global__ void __launch_bounds__(Eng::kBlock)
+    long_rows_plain_kernel(Eng eng, PassArgs a, const cx<T>* work, cx<T>* out,
+                           const cx<T>* __restrict__ tw2) {
+  long_rows_body<Eng, T>(eng, a, work, [&](long long l, int p, cx<T> v) { out[l * a.stride + p] = v; },
+                         tw2);
+}
+
+// Engines of the four-step passes: the power-of-two compile-time engines and
+// the run-time engine (the factors are short with radices <= 13, long_plan).
+// The mixed-radix compile-time engines are left out: with every IO variant in
+// each pass kernel, 25 more engine instantiations tripled the compile time.
+inline bool long_ct_factor(int n) { return n >= 16 && n <= 1024 && (n & (n - 1)) == 0; }
+template <typename T, int S, class F>
+inline void with_long_engine(int n, F&& f) {
+  switch (n) {
+#define SPFFT_LONG_CASE(NN)                                     \
+  case NN: {                                                     \
+    using E = CtEng<T, NN, S, true, true>;                       \
+    f(E{}, E::h_threads(), E::h_lines(), E::h_lds());            \
+    return;                                                      \
+  }
+    SPFFT_LONG_CASE(16)
+    SPFFT_LONG_CASE(32)
+    SPFFT_LONG_CASE(64)
+    SPFFT_LONG_CASE(128)
+    SPFFT_LONG_CASE(256)
+    SPFFT_LONG_CASE(512)
+    SPFFT_LONG_CASE(1024)
+#undef SPFFT_LONG_CASE
+    default: {
+      RtEng<T, S, true> e{make_rt_plan(n, sizeof(cx<T>))};
+      f(e, kRtThreads, e.p.lines, std::size_t(e.p.inplace ? 1 : 2) * e.p.lines * e.p.ls * sizeof(cx<T>));
+    }
   }
 }
 
-// length n1 * n2 lines: src (destroyed) -> dst, natural order both sides
-template <typename T, int S>
-void four_step(const LongPlan& lp, cx<T>* src, long long srcStride, cx<T>* dst, long long dstStride,
-               long long lines, hipStream_t stream) {
+// length n1 * n2 lines: io.load -> io.store, through `work` (lines * n1 * n2
+// elements; may be the load's own buffer: a columns workgroup stages all of its
+// elements before it writes them back). Run-time engine passes take a glue pass
+// instead of the fused IO; `scratch` (lines * n1 * n2) holds the rows pass
+// output for it.
+template <typename T, typename BT, int S>
+void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<T>* work,
+               cx<T>* scratch, hipStream_t stream, int fence = 0) {
   if (lines <= 0) return;
-  with_engine<T, S, true>(lp.n1, [&](auto eng, int threads, int B, std::size_t lds) {
-    PassArgs a{lp.n1, lp.n2, srcStride, srcStride, static_cast<int>(ceil_div(lp.n2, B))};
-    auto k = long_cols_kernel<decltype(eng), T, S>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(lines * a.blocksPerLine)), dim3(threads), lds,
-                       stream, eng, a, src, static_cast<const cx<T>*>(lp.tw1),
-                       static_cast<const cx<T>*>(lp.twM));
+  const long long stride = static_cast<long long>(lp.n1) * lp.n2;
+  const bool ct1 = long_ct_factor(lp.n1), ct2 = long_ct_factor(lp.n2);
+  if (!ct1) {
+    const LongIO<T, BT> l = io;
+    for_each(lines * stride, stream, [=] __device__(long long i) {
+      const long long line = i / stride;
+      work[i] = l.load(line, static_cast<int>(i - line * stride));
+    });
+  }
+  with_long_engine<T, S>(lp.n1, [&](auto eng, int threads, int B, std::size_t lds) {
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n2, B)), 0};
+    const dim3 grid(static_cast<unsigned>(lines * a.blocksPerLine));
+    const auto* tw1 = static_cast<const cx<T>*>(lp.tw1);
+    const auto* twM = static_cast<const cx<T>*>(lp.twM);
+    if constexpr (decltype(eng)::kBatchedCopy) {
+      auto k = long_cols_plain_kernel<decltype(eng), T, S>;
+      prepare_kernel(k, lds);
+      hipLaunchKernelGGL(k, grid, dim3(threads), lds, stream, eng, a, work, tw1, twM);
+    } else {
+      auto k = long_cols_kernel<decltype(eng), T, BT, S>;
+      prepare_kernel(k, lds);
+      hipLaunchKernelGGL(k, grid, dim3(threads), lds, stream, eng, a, io, work, tw1, twM);
+    }
     gpu_check_launch("long_cols", stream);
   });
-  with_engine<T, S, true>(lp.n2, [&](auto eng, int threads, int B, std::size_t lds) {
-    PassArgs a{lp.n1, lp.n2, srcStride, dstStride, static_cast<int>(ceil_div(lp.n1, B))};
-    auto k = long_rows_kernel<decltype(eng), T, S>;
-    prepare_kernel(k, lds);
-    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(lines * a.blocksPerLine)), dim3(threads), lds,
-                       stream, eng, a, src, dst, static_cast<const cx<T>*>(lp.tw2));
+  with_long_engine<T, S>(lp.n2, [&](auto eng, int threads, int B, std::size_t lds) {
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n1, B)), ct2 ? fence : 0};
+    const dim3 grid(static_cast<unsigned>(lines * a.blocksPerLine));
+    const auto* tw2 = static_cast<const cx<T>*>(lp.tw2);
+    if constexpr (decltype(eng)::kBatchedCopy) {
+      auto k = long_rows_plain_kernel<decltype(eng), T, S>;
+      prepare_kernel(k, lds);
+      hipLaunchKernelGGL(k, grid, dim3(threads), lds, stream, eng, a, work, scratch, tw2);
+    } else {
+      auto k = long_rows_kernel<decltype(eng), T, BT, S>;
+      prepare_kernel(k, lds);
+      hipLaunchKernelGGL(k, grid, dim3(threads), lds, stream, eng, a, work, io, tw2);
+    }
     gpu_check_launch("long_rows", stream);
   });
+  if (!ct2) {
+    const LongIO<T, BT> l = io;
+    const cx<T>* res = scratch;
+    for_each(lines * stride, stream, [=] __device__(long long i) {
+      const long long line = i / stride;
+      l.store(line, static_cast<int>(i - line * stride), res[i]);
+    }, fence);
+  }
 }
 
-// one long FFT of sign S over `lines` lines: src (destroyed) -> dst
-template <typename T, int S>
-void long_fft(const LongPlan& lp, cx<T>* src, long long srcStride, cx<T>* dst, long long dstStride,
-              long long lines, const LongBufs<T>& w, hipStream_t stream) {
+// One long FFT of sign S over `lines` lines of length lp.n: io.load -> io.store.
+// Bluestein (X_k = d_k sum_j (x_j d_j) conj(d_{k-j}), d_j = exp(S i pi j^2 / n))
+// runs as two four-steps of length m: the chirp folds into the first columns
+// pass's loads, the filter into its rows pass's stores, the final chirp and
+// 1/m into the second rows pass's stores: four kernels, no glue.
+template <typename T, typename BT, int S>
+void long_fft(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, const LongBufs<T>& w,
+              hipStream_t stream, int fence = 0) {
   if (!lp.bluestein) {
-    four_step<T, S>(lp, src, srcStride, dst, dstStride, lines, stream);
+    four_step<T, BT, S>(lp, lines, io, w.in, w.out, stream, fence);
     return;
   }
-  // X_k = d_k sum_j (x_j d_j) conj(d_{k-j}) (d_j = exp(S i pi j^2 / n)): one
-  // cyclic convolution of length m through FFT_m(-1), the filter, FFT_m(+1)
-  const int n = lp.n, m = lp.m;
+  const int m = lp.m;
   const cx<T>* chirp = static_cast<const cx<T>*>(lp.chirp);
-  const cx<T>* filt = static_cast<const cx<T>*>(lp.filt) + (S < 0 ? 0 : m);
-  cx<T>* w1 = w.w1;
-  cx<T>* w2 = w.w2;
-  for_each(lines * m, stream, [=] __device__(long long i) {
-    const long long l = i / m;
-    const int j = static_cast<int>(i - l * m);
-    cx<T> v = czero<T>();
-    if (j < n) {
-      const cx<T> d = S < 0 ? chirp[j] : conj(chirp[j]);
-      v = cmul(src[l * srcStride + j], d);
-    }
-    w1[i] = v;
-  });
-  four_step<T, -1>(lp, w1, m, w2, m, lines, stream);
-  for_each(lines * m, stream, [=] __device__(long long i) {
-    const int j = static_cast<int>(i % m);
-    w2[i] = cmul(w2[i], filt[j]);
-  });
-  four_step<T, +1>(lp, w2, m, w1, m, lines, stream);
-  const T inv = T(1) / static_cast<T>(m);
-  for_each(lines * n, stream, [=] __device__(long long i) {
-    const long long l = i / n;
-    const int k = static_cast<int>(i - l * n);
-    const cx<T> d = S < 0 ? chirp[k] : conj(chirp[k]);
-    dst[l * dstStride + k] = scale(cmul(w1[l * m + k], d), inv);
-  });
+  LongIO<T, BT> first = io;  // the stage's load with the chirp; store: the filter product
+  first.chirpIn = chirp;
+  first.chirpN = lp.n;
+  first.chirpConj = S < 0 ? 0 : 1;
+  first.sk = LongIO<T, BT>::kFilter;
+  first.chirpOut = nullptr;
+  first.dst = w.w2;
+  first.dstStride = m;
+  first.filt = static_cast<const cx<T>*>(lp.filt) + (S < 0 ? 0 : m);
+  four_step<T, BT, -1>(lp, lines, first, w.w1, w.out, stream);
+  LongIO<T, BT> second = io;  // load: the convolution; the stage's store with the chirp
+  second.lk = LongIO<T, BT>::kPlain;
+  second.chirpIn = nullptr;
+  second.src = w.w2;
+  second.srcStride = m;
+  second.chirpOut = chirp;
+  second.chirpN = lp.n;
+  second.chirpConj = S < 0 ? 0 : 1;
+  second.outScale = T(1) / static_cast<T>(m);
+  four_step<T, BT, +1>(lp, lines, second, w.w2, w.out, stream, fence);
 }
 
 // ------------------------------------------------------------ plans
@@ -196,7 +466,7 @@ int largest_prime(int n) {
 }
 // a factor the one-workgroup engines run well (compile-time, or run-time with
 // codelet radices only)
-bool short_ok(int f) { return has_ct_kernel(f) || (f >= 2 && f <= 4096 && largest_prime(f) <= 13); }
+bool short_ok(int f) { return long_ct_factor(f) || (f >= 2 && f <= 4096 && largest_prime(f) <= 13); }
 
 template <typename T>
 void bluestein_host_tables(int n, int m, std::vector<cx<T>>& chirp, std::vector<cx<T>>& filt) {
@@ -249,7 +519,7 @@ LongPlan long_plan(int n, bool dbl) {
   int best = -1, bestScore = 1 << 30;
   for (int d = 2; d <= n / 2; ++d) {
     if (n % d || !short_ok(d) || !short_ok(n / d)) continue;
-    const int score = ((has_ct_kernel(d) ? 0 : 1) + (has_ct_kernel(n / d) ? 0 : 1)) * (1 << 20) +
+    const int score = ((long_ct_factor(d) ? 0 : 1) + (long_ct_factor(n / d) ? 0 : 1)) * (1 << 20) +
                       std::abs(d - n / d);
     if (score < bestScore) {
       bestScore = score;
@@ -307,6 +577,10 @@ LongPlan long_plan(int n, bool dbl) {
 }
 
 // ------------------------------------------------------------ z stage
+// Fused when every stick is simple (StickDesc: at most two z-runs of contiguous
+// values): the columns pass gathers the sparse values itself (with the (0,0)
+// stick's hermitian fill) and the rows pass stores into the exchange layout.
+// Other index sets stage the decompressed sticks in natural order first.
 template <typename T, typename BT>
 void launch_long_z_backward(const LongPlan& lp, const ZArgs& a, const cx<T>* values, BT* out,
                             const LongBufs<T>& w, hipStream_t stream) {
@@ -314,15 +588,27 @@ void launch_long_z_backward(const LongPlan& lp, const ZArgs& a, const cx<T>* val
   if (S <= 0) return;
   const int n = a.n;
   const int s0 = a.stickBegin;
-  cx<T>* in = w.in;
+  LongIO<T, BT> io;
+  io.n = n;
+  io.zSingle = a.single;
+  io.zStride = a.stickStride;
+  io.zTab = a.zTab;
+  io.s0 = s0;
+  io.sk = LongIO<T, BT>::kZSeg;
+  io.xout = out;
+  if (a.desc) {
+    io.lk = LongIO<T, BT>::kZValues;
+    io.desc = a.desc;
+    io.values = values;
+    io.zeroStick = a.zeroStick;
+    long_fft<T, BT, +1>(lp, S, io, w, stream, a.remote);
+    return;
+  }
+  cx<T>* in = w.out;
   gpu_check(hipMemsetAsync(in, 0, static_cast<std::size_t>(S) * n * sizeof(cx<T>), stream),
             "hipMemsetAsync");
-  // decompress: one thread per run
   const StickRun* runs = a.runs;
-  const int q0 = 0;
-  (void)q0;
   const int* ro = a.runOffsets;
-  // the run range of the sticks [s0, numSticks) is read on the device
   for_each(S, stream, [=] __device__(long long s) {
     const int st = s0 + static_cast<int>(s);
     for (int q = ro[st]; q < ro[st + 1]; ++q) {
@@ -336,14 +622,10 @@ void launch_long_z_backward(const LongPlan& lp, const ZArgs& a, const cx<T>* val
                        in + static_cast<long long>(a.zeroStick - s0) * n, static_cast<long long>(n), n);
     gpu_check_launch("long_herm", stream);
   }
-  long_fft<T, +1>(lp, in, n, w.out, n, S, w, stream);
-  const cx<T>* res = w.out;
-  const ZArgs za = a;
-  for_each(S * n, stream, [=] __device__(long long i) {
-    const long long s = i / n;
-    const int z = static_cast<int>(i - s * n);
-    out[seg_index(za, s0 + static_cast<int>(s), z)] = cvt<typename BT::value_type>(res[i]);
-  }, a.remote);
+  io.lk = LongIO<T, BT>::kPlain;
+  io.src = in;
+  io.srcStride = n;
+  long_fft<T, BT, +1>(lp, S, io, w, stream, a.remote);
 }
 
 template <typename T, typename BT>
@@ -353,15 +635,27 @@ void launch_long_z_forward(const LongPlan& lp, const ZArgs& a, const BT* in, cx<
   if (S <= 0) return;
   const int n = a.n;
   const int s0 = a.stickBegin;
-  cx<T>* lines = w.in;
-  const ZArgs za = a;
-  for_each(S * n, stream, [=] __device__(long long i) {
-    const long long s = i / n;
-    const int z = static_cast<int>(i - s * n);
-    lines[i] = cvt<T>(in[seg_index(za, s0 + static_cast<int>(s), z)]);
-  });
-  long_fft<T, -1>(lp, lines, n, w.out, n, S, w, stream);
-  const cx<T>* res = w.out;
+  LongIO<T, BT> io;
+  io.n = n;
+  io.zSingle = a.single;
+  io.zStride = a.stickStride;
+  io.zTab = a.zTab;
+  io.s0 = s0;
+  io.lk = LongIO<T, BT>::kZSeg;
+  io.xin = in;
+  if (a.desc) {
+    io.sk = LongIO<T, BT>::kZValues;
+    io.desc = a.desc;
+    io.valuesOut = values;
+    io.vscale = scl;
+    long_fft<T, BT, -1>(lp, S, io, w, stream);
+    return;
+  }
+  cx<T>* res = w.out;
+  io.sk = LongIO<T, BT>::kPlain;
+  io.dst = res;
+  io.dstStride = n;
+  long_fft<T, BT, -1>(lp, S, io, w, stream);
   const StickRun* runs = a.runs;
   const int* ro = a.runOffsets;
   for_each(S, stream, [=] __device__(long long s) {
@@ -375,6 +669,9 @@ void launch_long_z_forward(const LongPlan& lp, const ZArgs& a, const BT* in, cx<
 }
 
 // ------------------------------------------------------------ y stage
+// Fused when the plan has column run descriptors (YArgs::colDesc): the columns
+// pass gathers the stick entries of a column (with the x = 0 column's
+// hermitian fill), the forward rows pass stores into them.
 template <typename T, typename BT>
 void launch_long_y_backward(const LongPlan& lp, const YArgs& a, const BT* in, cx<T>* inter,
                             const LongBufs<T>& w, hipStream_t stream) {
@@ -382,7 +679,24 @@ void launch_long_y_backward(const LongPlan& lp, const YArgs& a, const BT* in, cx
   const int C = a.ncols, n = a.n, zb = a.zBegin;
   if (nz <= 0 || C <= 0) return;
   const long long lines = static_cast<long long>(nz) * C;
-  cx<T>* lin = w.in;
+  LongIO<T, BT> io;
+  io.n = n;
+  // line l = (plane zz, column c) -> row (zb + zz, c) of [z][column][y]
+  io.sk = LongIO<T, BT>::kPlain;
+  io.dst = inter + zb * a.interZStride;
+  io.dstStride = a.interStride;
+  if (a.colDesc) {
+    io.lk = LongIO<T, BT>::kYCols;
+    io.colDesc = a.colDesc;
+    io.colStride = a.colStride;
+    io.xin = in;
+    io.zb = zb;
+    io.C = C;
+    io.x0 = a.colOfX0;
+    long_fft<T, BT, +1>(lp, lines, io, w, stream);
+    return;
+  }
+  cx<T>* lin = w.out;
   gpu_check(hipMemsetAsync(lin, 0, static_cast<std::size_t>(lines) * n * sizeof(cx<T>), stream),
             "hipMemsetAsync");
   const int* co = a.colOffsets;
@@ -398,7 +712,10 @@ void launch_long_y_backward(const LongPlan& lp, const YArgs& a, const BT* in, cx
                        lin + static_cast<long long>(a.colOfX0) * n, static_cast<long long>(C) * n, n);
     gpu_check_launch("long_herm", stream);
   }
-  long_fft<T, +1>(lp, lin, n, inter + zb * a.interZStride, a.interStride, lines, w, stream);
+  io.lk = LongIO<T, BT>::kPlain;
+  io.src = lin;
+  io.srcStride = n;
+  long_fft<T, BT, +1>(lp, lines, io, w, stream);
 }
 
 template <typename T, typename BT>
@@ -408,8 +725,26 @@ void launch_long_y_forward(const LongPlan& lp, const YArgs& a, cx<T>* inter, BT*
   const int C = a.ncols, n = a.n, zb = a.zBegin;
   if (nz <= 0 || C <= 0) return;
   const long long lines = static_cast<long long>(nz) * C;
-  long_fft<T, -1>(lp, inter + zb * a.interZStride, a.interStride, w.out, n, lines, w, stream);
-  const cx<T>* res = w.out;
+  LongIO<T, BT> io;
+  io.n = n;
+  io.lk = LongIO<T, BT>::kPlain;
+  io.src = inter + zb * a.interZStride;
+  io.srcStride = a.interStride;
+  if (a.colDesc) {
+    io.sk = LongIO<T, BT>::kYCols;
+    io.colDesc = a.colDesc;
+    io.colStride = a.colStride;
+    io.xout = out;
+    io.zb = zb;
+    io.C = C;
+    long_fft<T, BT, -1>(lp, lines, io, w, stream, a.remote);
+    return;
+  }
+  cx<T>* res = w.out;
+  io.sk = LongIO<T, BT>::kPlain;
+  io.dst = res;
+  io.dstStride = n;
+  long_fft<T, BT, -1>(lp, lines, io, w, stream);
   const int* co = a.colOffsets;
   const int* cy = a.colY;
   const long long* cb = a.colBase;
@@ -422,66 +757,49 @@ void launch_long_y_forward(const LongPlan& lp, const YArgs& a, cx<T>* inter, BT*
 }
 
 // ------------------------------------------------------------ x stage
+// Fused: the columns pass reads the intermediate's columns through the x ->
+// column table (XArgs::xToCol; the packed-real C2R pre-pass and the odd-length
+// C2R mirror folded into the load), the rows pass writes the space rows; the
+// forward rows pass stores the columns that hold sticks (C2C and odd R2C; the
+// packed R2C post-pass pairs outputs k and h - k of one line and keeps its glue).
 template <typename T>
 void launch_long_x_backward(const LongPlan& lp, const XArgs& a, bool r2c, const cx<T>* inter,
                             void* space, const cx<T>* twFull, const LongBufs<T>& w,
                             hipStream_t stream) {
   const int nz = a.L - a.zBegin;
-  const int Y = a.Y, X = a.n, C = a.ncols, zb = a.zBegin;
+  const int Y = a.Y, X = a.n, zb = a.zBegin;
   if (nz <= 0 || Y <= 0) return;
   const long long lines = static_cast<long long>(nz) * Y;
-  const long long iz = a.interZStride, is = a.interStride;
-  const int* colX = a.colX;
-  const cx<T>* src = inter + zb * iz;
-  auto scatter_cols = [&](cx<T>* dst, int rowLen) {
-    gpu_check(hipMemsetAsync(dst, 0, static_cast<std::size_t>(lines) * rowLen * sizeof(cx<T>), stream),
-              "hipMemsetAsync");
-    for_each(lines * C, stream, [=] __device__(long long i) {
-      const long long l = i / C;
-      const int c = static_cast<int>(i - l * C);
-      const long long zz = l / Y, y = l - zz * Y;
-      dst[l * rowLen + colX[c]] = src[zz * iz + c * is + y];
-    });
-  };
+  LongIO<T, cx<T>> io;
+  io.inter = inter + zb * a.interZStride;
+  io.iz = a.interZStride;
+  io.is = a.interStride;
+  io.Y = Y;
+  io.X = X;
+  io.nf = a.nFreq;
+  io.xToCol = a.xToCol;
+  io.twFull = twFull;
   if (!r2c) {
-    scatter_cols(w.in, X);
-    long_fft<T, +1>(lp, w.in, X, static_cast<cx<T>*>(space) + static_cast<long long>(zb) * Y * X, X,
-                    lines, w, stream);
+    io.n = X;
+    io.lk = LongIO<T, cx<T>>::kXCols;
+    io.dst = static_cast<cx<T>*>(space) + static_cast<long long>(zb) * Y * X;
+    io.dstStride = X;
   } else if (X % 2 == 0) {
     // packed real rows: Z[k] = (X[k] + conj X[h-k]) + i (X[k] - conj X[h-k]) w^k,
     // w = exp(+2 pi i / X), imaginary parts of X[0], X[h] ignored; IDFT_h(Z)
     // interleaves the real row
-    const int h = X / 2;
-    cx<T>* half = w.out;  // X[0..h] per line (stride h + 1)
-    scatter_cols(half, h + 1);
-    cx<T>* z = w.in;
-    for_each(lines * h, stream, [=] __device__(long long i) {
-      const long long l = i / h;
-      const int k = static_cast<int>(i - l * h);
-      cx<T> xk = half[l * (h + 1) + k], xm = half[l * (h + 1) + (h - k)];
-      if (k == 0) {
-        xk.y = T(0);
-        xm.y = T(0);
-      }
-      const cx<T> xmc = conj(xm);
-      z[i] = (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twFull[k]));
-    });
-    long_fft<T, +1>(lp, z, h, reinterpret_cast<cx<T>*>(static_cast<T*>(space) + static_cast<long long>(zb) * Y * X), h,
-                    lines, w, stream);
+    io.h = X / 2;
+    io.n = io.h;
+    io.lk = LongIO<T, cx<T>>::kXPacked;
+    io.dst = reinterpret_cast<cx<T>*>(static_cast<T*>(space) + static_cast<long long>(zb) * Y * X);
+    io.dstStride = io.h;
   } else {
-    const int nf = a.nFreq;
-    cx<T>* full = w.in;
-    scatter_cols(full, X);
-    for_each(lines * X, stream, [=] __device__(long long i) {
-      const long long l = i / X;
-      const int x = static_cast<int>(i - l * X);
-      if (x >= nf) full[i] = conj(full[l * X + (X - x)]);
-    });
-    long_fft<T, +1>(lp, full, X, w.out, X, lines, w, stream);
-    const cx<T>* res = w.out;
-    T* dst = static_cast<T*>(space) + static_cast<long long>(zb) * Y * X;
-    for_each(lines * X, stream, [=] __device__(long long i) { dst[i] = res[i].x; });
+    io.n = X;
+    io.lk = LongIO<T, cx<T>>::kXOdd;
+    io.sk = LongIO<T, cx<T>>::kReal;
+    io.realDst = static_cast<T*>(space) + static_cast<long long>(zb) * Y * X;
   }
+  long_fft<T, cx<T>, +1>(lp, lines, io, w, stream);
 }
 
 template <typename T>
@@ -493,34 +811,37 @@ void launch_long_x_forward(const LongPlan& lp, const XArgs& a, bool r2c, const v
   if (nz <= 0 || Y <= 0) return;
   const long long lines = static_cast<long long>(nz) * Y;
   const long long iz = a.interZStride, is = a.interStride;
-  const int* colX = a.colX;
   cx<T>* dst = inter + zb * iz;
-  auto gather_cols = [&](const cx<T>* res, int rowLen) {
-    for_each(lines * C, stream, [=] __device__(long long i) {
-      const long long l = i / C;
-      const int c = static_cast<int>(i - l * C);
-      const long long zz = l / Y, y = l - zz * Y;
-      dst[zz * iz + c * is + y] = res[l * rowLen + colX[c]];
-    });
-  };
+  LongIO<T, cx<T>> io;
+  io.interOut = dst;
+  io.iz = iz;
+  io.is = is;
+  io.Y = Y;
+  io.X = X;
+  io.nf = a.nFreq;
+  io.xToCol = a.xToCol;
+  io.sk = LongIO<T, cx<T>>::kXPut;
   if (!r2c) {
-    // the space domain stays intact: the four-step destroys its input
-    gpu_check(hipMemcpyAsync(w.in, static_cast<const cx<T>*>(space) + static_cast<long long>(zb) * Y * X,
-                             static_cast<std::size_t>(lines) * X * sizeof(cx<T>),
-                             hipMemcpyDeviceToDevice, stream),
-              "hipMemcpyAsync");
-    long_fft<T, -1>(lp, w.in, X, w.out, X, lines, w, stream);
-    gather_cols(w.out, X);
+    // (the four-step works in its own buffer: the space domain stays intact)
+    io.n = X;
+    io.lk = LongIO<T, cx<T>>::kPlain;
+    io.src = static_cast<const cx<T>*>(space) + static_cast<long long>(zb) * Y * X;
+    io.srcStride = X;
+    long_fft<T, cx<T>, -1>(lp, lines, io, w, stream);
   } else if (X % 2 == 0) {
     // packed real rows y[m] = x[2m] + i x[2m+1]: X[k] = (Y[k] + conj Y[h-k]) / 2
     // + w^k (Y[k] - conj Y[h-k]) / (2i), w = exp(-2 pi i / X), Y[h] = Y[0]
     const int h = X / 2;
-    gpu_check(hipMemcpyAsync(w.in, static_cast<const T*>(space) + static_cast<long long>(zb) * Y * X,
-                             static_cast<std::size_t>(lines) * X * sizeof(T), hipMemcpyDeviceToDevice,
-                             stream),
-              "hipMemcpyAsync");
-    long_fft<T, -1>(lp, w.in, h, w.out, h, lines, w, stream);
-    const cx<T>* res = w.out;
+    io.n = h;
+    io.lk = LongIO<T, cx<T>>::kPlain;
+    io.src = reinterpret_cast<const cx<T>*>(static_cast<const T*>(space) + static_cast<long long>(zb) * Y * X);
+    io.srcStride = h;
+    cx<T>* res = w.out;
+    io.sk = LongIO<T, cx<T>>::kPlain;
+    io.dst = res;
+    io.dstStride = h;
+    long_fft<T, cx<T>, -1>(lp, lines, io, w, stream);
+    const int* colX = a.colX;
     for_each(lines * C, stream, [=] __device__(long long i) {
       const long long l = i / C;
       const int c = static_cast<int>(i - l * C);
@@ -533,11 +854,10 @@ void launch_long_x_forward(const LongPlan& lp, const XArgs& a, bool r2c, const v
       dst[zz * iz + c * is + y] = e + twm<-1>(o, twFull[k]);
     });
   } else {
-    const T* sp = static_cast<const T*>(space) + static_cast<long long>(zb) * Y * X;
-    cx<T>* lin = w.in;
-    for_each(lines * X, stream, [=] __device__(long long i) { lin[i] = mk<T>(sp[i], T(0)); });
-    long_fft<T, -1>(lp, lin, X, w.out, X, lines, w, stream);
-    gather_cols(w.out, X);
+    io.n = X;
+    io.lk = LongIO<T, cx<T>>::kXReal;
+    io.realSrc = static_cast<const T*>(space) + static_cast<long long>(zb) * Y * X;
+    long_fft<T, cx<T>, -1>(lp, lines, io, w, stream);
   }
 }
 

@@ -96,6 +96,7 @@ struct XArgs {
   long long interStride;  // row stride of the [z][column][y] intermediate (>= Y)
   long long interZStride;  // as YArgs
   const int* colX;
+  const int* xToCol;  // nFreq entries: x -> column or -1 (long-line x stage)
   BatchPtrs batch;
 };
 

@@ -143,25 +143,25 @@ struct CtEng {
   static constexpr bool kBatchedCopy = false;
   static constexpr bool kLineFast = LF;
   static constexpr int kBlock = F::NT > kMaxThreads ? F::NT : kMaxThreads;
-  __device__ int lines() const { return F::B; }
-  __device__ int n() const { return N; }
-  __device__ int in_at(int b, int pos) const { return F::in_at(b, pos); }
-  __device__ int out_at(int b, int pos) const { return F::out_at(b, pos); }
-  __device__ int input_elems() const { return F::B * F::LS; }
-  __device__ int lds_bytes() const { return static_cast<int>(F::lds_bytes()); }
+  __device__ __forceinline__ int lines() const { return F::B; }
+  __device__ __forceinline__ int n() const { return N; }
+  __device__ __forceinline__ int in_at(int b, int pos) const { return F::in_at(b, pos); }
+  __device__ __forceinline__ int out_at(int b, int pos) const { return F::out_at(b, pos); }
+  __device__ __forceinline__ int input_elems() const { return F::B * F::LS; }
+  __device__ __forceinline__ int lds_bytes() const { return static_cast<int>(F::lds_bytes()); }
   template <class St>
-  __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
+  __device__ __forceinline__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     F::run(lds, tw, NoLoad{}, st);
   }
   template <class Ld>
-  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
+  __device__ __forceinline__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
     F::run_to_lds(lds, tw, ld);
   }
-  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
+  __device__ __forceinline__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
     F::run_to_lds(lds, tw, NoLoad{});
   }
   template <class Ld, class St>
-  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+  __device__ __forceinline__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
     F::run(lds, tw, ld, st);
   }
   // host side
@@ -180,20 +180,20 @@ struct RtEng {
   static constexpr bool kLineFast = LF;
   static constexpr int kBlock = kRtThreads;
   RtPlan p;
-  __device__ int lines() const { return p.lines; }
-  __device__ int n() const { return p.n; }
-  __device__ int in_at(int b, int pos) const { return b * p.ls + pos; }
-  __device__ int out_at(int b, int pos) const {
+  __device__ __forceinline__ int lines() const { return p.lines; }
+  __device__ __forceinline__ int n() const { return p.n; }
+  __device__ __forceinline__ int in_at(int b, int pos) const { return b * p.ls + pos; }
+  __device__ __forceinline__ int out_at(int b, int pos) const {
     return ((!p.inplace && (p.np & 1)) ? p.lines * p.ls : 0) + b * p.ls + pos;
   }
-  __device__ int input_elems() const { return p.lines * p.ls; }
-  __device__ int lds_bytes() const {
+  __device__ __forceinline__ int input_elems() const { return p.lines * p.ls; }
+  __device__ __forceinline__ int lds_bytes() const {
     return (p.inplace ? 1 : 2) * p.lines * p.ls * static_cast<int>(sizeof(cx<T>));
   }
   // global-side element idx -> (line b, position pos); plan lines are a power
   // of two (make_rt_plan), so the line-fast split is a mask and a shift, and
   // the row split divides by a precomputed reciprocal
-  __device__ void split(int idx, int& b, int& pos) const {
+  __device__ __forceinline__ void split(int idx, int& b, int& pos) const {
     if (LF) {
       b = idx & (p.lines - 1);
       pos = idx >> p.linesLog2;
@@ -203,14 +203,14 @@ struct RtEng {
     }
   }
   template <class St>
-  __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
+  __device__ __forceinline__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, St st) const {
     const cx<T>* res = FftRT<T, S>::run_in_lds(p, lds, tw);
     store_from(res, st);
   }
   // input -> LDS at in_at(b, pos), no barrier (kernels with several input
   // paths stage each and then run the FFT once: one inlined copy of the passes)
   template <class Ld>
-  __device__ void stage(cx<T>* lds, Ld ld) const {
+  __device__ __forceinline__ void stage(cx<T>* lds, Ld ld) const {
     gather_to_lds(lds, p.lines * p.n, [&](int idx) {
       int b, pos;
       split(idx, b, pos);
@@ -222,22 +222,22 @@ struct RtEng {
     });
   }
   template <class Ld>
-  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
+  __device__ __forceinline__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld) const {
     stage(lds, ld);
     __syncthreads();
     FftRT<T, S>::run_in_lds(p, lds, tw);
   }
-  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
+  __device__ __forceinline__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__ tw) const {
     FftRT<T, S>::run_in_lds(p, lds, tw);
   }
   template <class Ld, class St>
-  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+  __device__ __forceinline__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
     global_to_lds(lds, tw, ld);
     store_from(lds + out_at(0, 0), st);
   }
   // result region res (index b * ls + pos) -> st(b, pos, v)
   template <class St>
-  __device__ void store_from(const cx<T>* res, St st) const {
+  __device__ __forceinline__ void store_from(const cx<T>* res, St st) const {
     scatter_from_lds(res, p.lines * p.n, [&](int idx) {
       int b, pos;
       split(idx, b, pos);
@@ -265,14 +265,14 @@ struct BlueEng {
   const cx<T>* chirp;
   const cx<T>* filt;
   const cx<T>* twm;
-  __device__ int lines() const { return pm.lines; }
-  __device__ int n() const { return nn; }
-  __device__ int in_at(int b, int pos) const { return b * pm.ls + pos; }
-  __device__ int out_at(int b, int pos) const { return b * pm.ls + pos; }
-  __device__ int input_elems() const { return pm.lines * pm.ls; }
-  __device__ int lds_bytes() const { return 2 * pm.lines * pm.ls * static_cast<int>(sizeof(cx<T>)); }
-  __device__ cx<T> d(int j) const { return S < 0 ? chirp[j] : conj(chirp[j]); }
-  __device__ void run(cx<T>* lds) const {
+  __device__ __forceinline__ int lines() const { return pm.lines; }
+  __device__ __forceinline__ int n() const { return nn; }
+  __device__ __forceinline__ int in_at(int b, int pos) const { return b * pm.ls + pos; }
+  __device__ __forceinline__ int out_at(int b, int pos) const { return b * pm.ls + pos; }
+  __device__ __forceinline__ int input_elems() const { return pm.lines * pm.ls; }
+  __device__ __forceinline__ int lds_bytes() const { return 2 * pm.lines * pm.ls * static_cast<int>(sizeof(cx<T>)); }
+  __device__ __forceinline__ cx<T> d(int j) const { return S < 0 ? chirp[j] : conj(chirp[j]); }
+  __device__ __forceinline__ void run(cx<T>* lds) const {
     const int m = pm.n, total = pm.lines * m;
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
       const int b = idx / m, j = idx - b * m;
@@ -298,12 +298,12 @@ struct BlueEng {
     __syncthreads();
   }
   template <class St>
-  __device__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__, St st) const {
+  __device__ __forceinline__ void lds_to_global(cx<T>* lds, const cx<T>* __restrict__, St st) const {
     run(lds);
     store_from(lds, st);
   }
   template <class Ld>
-  __device__ void stage(cx<T>* lds, Ld ld) const {
+  __device__ __forceinline__ void stage(cx<T>* lds, Ld ld) const {
     gather_to_lds(lds, pm.lines * nn, [&](int idx) {
       const int b = idx / nn;
       return ld(b, idx - b * nn);
@@ -313,19 +313,19 @@ struct BlueEng {
     });
   }
   template <class Ld>
-  __device__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
+  __device__ __forceinline__ void global_to_lds(cx<T>* lds, const cx<T>* __restrict__, Ld ld) const {
     stage(lds, ld);
     __syncthreads();
     run(lds);
   }
-  __device__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__) const { run(lds); }
+  __device__ __forceinline__ void lds_to_lds(cx<T>* lds, const cx<T>* __restrict__) const { run(lds); }
   template <class Ld, class St>
-  __device__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
+  __device__ __forceinline__ void global_to_global(cx<T>* lds, const cx<T>* __restrict__ tw, Ld ld, St st) const {
     global_to_lds(lds, tw, ld);
     store_from(lds, st);
   }
   template <class St>
-  __device__ void store_from(const cx<T>* lds, St st) const {
+  __device__ __forceinline__ void store_from(const cx<T>* lds, St st) const {
     scatter_from_lds(lds, pm.lines * nn, [&](int idx) {
       const int b = idx / nn;
       return out_at(b, idx - b * nn);
