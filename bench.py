@@ -348,7 +348,7 @@ def main():
                 "stage_ms": stages,
                 "stage_ms_basis": (f"transform 0 alone, median of {a.profile_reps} backward+forward "
                                    "pairs after the timed loop (hipEvent stage marks)" if stages else None),
-                "exchange": exch,
+                "exchange_stats": exch,
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),
             },

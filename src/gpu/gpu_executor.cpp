@@ -969,17 +969,18 @@ void GpuExecutor<T>::backward_exchange(bool /*nonBlocking*/) {
 
 // ------------------------------------------------------------- long axes
 // Axes longer than one workgroup's LDS (or with a large prime factor and no
-// in-LDS Bluestein) run glue kernel -> global four-step / Bluestein FFT ->
-// glue kernel instead of the fused stage kernel (kernels/long_fft.hpp).
+// in-LDS Bluestein, or line-fast axes whose run-time engine would hold less than
+// a column segment) run the global four-step / Bluestein FFT with the stage IO
+// fused into its passes (kernels/long_fft.hpp: needs_long_path).
 template <typename T>
 void GpuExecutor<T>::setup_long_axes() {
   const IndexPlan& p = *plan_;
   const bool dbl = sizeof(T) == 8;
   const bool packedX = p.type == SPFFT_TRANS_R2C && p.dimX % 2 == 0 && p.dimX >= 4;
   const int xLen = packedX ? p.dimX / 2 : p.dimX;
-  longZ_ = dev::needs_long_path(p.dimZ, dbl);
-  longY_ = dev::needs_long_path(p.dimY, dbl);
-  longX_ = dev::needs_long_path(xLen, dbl);
+  longZ_ = dev::needs_long_path(p.dimZ, dbl, dev::kLongAxisZ);
+  longY_ = dev::needs_long_path(p.dimY, dbl, dev::kLongAxisY);
+  longX_ = dev::needs_long_path(xLen, dbl, dev::kLongAxisX);
   long long elems = 0;
   if (longZ_) {
     lpZ_ = dev::long_plan(p.dimZ, dbl);

@@ -55,11 +55,19 @@ __global__ void __launch_bounds__(256) herm_lines_kernel(cx<T>* base, long long 
 }
 
 // ------------------------------------------------------------ four-step
+// A pass workgroup runs its engine's B lines on a tile of lt lines x (B / lt)
+// columns (cols pass: j2, rows pass: k1) of the [n1][n2] views; the B engine
+// lines run lines fastest. lt = 1 (one line) where the stage side is a row of
+// the line (sticks, rows of the intermediate or of the space domain); the x
+// stage's intermediate side ([z][column][y]: consecutive x are a column apart)
+// takes lt > 1, so its accesses cover lt consecutive y instead of one element.
 struct PassArgs {
   int n1, n2;
   long long stride;  // work buffer line stride
-  int blocksPerLine;
+  int blocksPerLine;  // tiles per line tile: ceil(n2 / (B / lt)) (cols), ceil(n1 / (B / lt)) (rows)
   int fence;  // rows pass: release its stores system-wide at exit (peer-write exchange)
+  int lt;     // lines per tile (a power of two dividing B)
+  long long lines;
 };
 
 // Value at position z of a line after the reference's two-pass hermitian
@@ -252,22 +260,24 @@ __device__ __forceinline__ void long_cols_body(const Eng& eng, const PassArgs& a
                                                int S) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const long long line = blockIdx.x / a.blocksPerLine;
-  const int j20 = static_cast<int>(blockIdx.x % a.blocksPerLine) * B;
-  cx<T>* base = work + line * a.stride;
+  const int lt = a.lt, ltShift = __builtin_ctz(static_cast<unsigned>(lt));
+  const long long l0 = static_cast<long long>(blockIdx.x / a.blocksPerLine) << ltShift;
+  const int j20 = static_cast<int>(blockIdx.x % a.blocksPerLine) * (B >> ltShift);
   const int total = B * a.n1;
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-    const int b = idx % B, j1 = idx / B, j2 = j20 + b;
-    lds[eng.in_at(b, j1)] = j2 < a.n2 ? src(line, j1 * a.n2 + j2) : czero<T>();
+    const int b = idx % B, j1 = idx / B, j2 = j20 + (b >> ltShift);
+    const long long line = l0 + (b & (lt - 1));
+    lds[eng.in_at(b, j1)] = (j2 < a.n2 && line < a.lines) ? src(line, j1 * a.n2 + j2) : czero<T>();
   }
   __syncthreads();
   eng.lds_to_lds(lds, tw1);
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-    const int b = idx % B, k1 = idx / B, j2 = j20 + b;
-    if (j2 < a.n2) {
+    const int b = idx % B, k1 = idx / B, j2 = j20 + (b >> ltShift);
+    const long long line = l0 + (b & (lt - 1));
+    if (j2 < a.n2 && line < a.lines) {
       const cx<T> w = twM[static_cast<long long>(j2) * k1];
       const cx<T> v = lds[eng.out_at(b, k1)];
-      base[static_cast<long long>(k1) * a.n2 + j2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
+      work[line * a.stride + static_cast<long long>(k1) * a.n2 + j2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
     }
   }
 }
@@ -293,19 +303,23 @@ __device__ __forceinline__ void long_rows_body(const Eng& eng, const PassArgs& a
                                                Dst dst, const cx<T>* __restrict__ tw2) {
   SPFFT_LDS_DECL(T);
   const int B = eng.lines();
-  const long long line = blockIdx.x / a.blocksPerLine;
-  const int k10 = static_cast<int>(blockIdx.x % a.blocksPerLine) * B;
-  const cx<T>* s = work + line * a.stride;
+  const int lt = a.lt, ltShift = __builtin_ctz(static_cast<unsigned>(lt));
+  const long long l0 = static_cast<long long>(blockIdx.x / a.blocksPerLine) << ltShift;
+  const int k10 = static_cast<int>(blockIdx.x % a.blocksPerLine) * (B >> ltShift);
   const int total = B * a.n2;
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-    const int b = idx / a.n2, j2 = idx - b * a.n2, k1 = k10 + b;
-    lds[eng.in_at(b, j2)] = k1 < a.n1 ? s[static_cast<long long>(k1) * a.n2 + j2] : czero<T>();
+    const int b = idx / a.n2, j2 = idx - b * a.n2, k1 = k10 + (b >> ltShift);
+    const long long line = l0 + (b & (lt - 1));
+    lds[eng.in_at(b, j2)] = (k1 < a.n1 && line < a.lines)
+                                ? work[line * a.stride + static_cast<long long>(k1) * a.n2 + j2]
+                                : czero<T>();
   }
   __syncthreads();
   eng.lds_to_lds(lds, tw2);
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-    const int b = idx % B, k2 = idx / B, k1 = k10 + b;
-    if (k1 < a.n1) dst(line, k1 + a.n1 * k2, lds[eng.out_at(b, k2)]);
+    const int b = idx % B, k2 = idx / B, k1 = k10 + (b >> ltShift);
+    const long long line = l0 + (b & (lt - 1));
+    if (k1 < a.n1 && line < a.lines) dst(line, k1 + a.n1 * k2, lds[eng.out_at(b, k2)]);
   }
   release_remote(a.fence);
 }
@@ -370,9 +384,15 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
       work[i] = l.load(line, static_cast<int>(i - line * stride));
     });
   }
+  // the x stage's intermediate side: tiles of several lines (consecutive y)
+  const auto tile = [](int B, bool xSide) { return xSide && B >= 8 ? B / 4 : 1; };
+  const bool xLoad = io.lk == LongIO<T, BT>::kXCols || io.lk == LongIO<T, BT>::kXPacked ||
+                     io.lk == LongIO<T, BT>::kXOdd;
+  const bool xStore = io.sk == LongIO<T, BT>::kXPut;
   with_long_engine<T, S>(lp.n1, [&](auto eng, int threads, int B, std::size_t lds) {
-    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n2, B)), 0};
-    const dim3 grid(static_cast<unsigned>(lines * a.blocksPerLine));
+    const int lt = decltype(eng)::kBatchedCopy ? 1 : tile(B, xLoad);
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n2, B / lt)), 0, lt, lines};
+    const dim3 grid(static_cast<unsigned>(ceil_div(lines, lt) * a.blocksPerLine));
     const auto* tw1 = static_cast<const cx<T>*>(lp.tw1);
     const auto* twM = static_cast<const cx<T>*>(lp.twM);
     if constexpr (decltype(eng)::kBatchedCopy) {
@@ -387,8 +407,10 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
     gpu_check_launch("long_cols", stream);
   });
   with_long_engine<T, S>(lp.n2, [&](auto eng, int threads, int B, std::size_t lds) {
-    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n1, B)), ct2 ? fence : 0};
-    const dim3 grid(static_cast<unsigned>(lines * a.blocksPerLine));
+    const int lt = decltype(eng)::kBatchedCopy ? 1 : tile(B, xStore);
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n1, B / lt)), ct2 ? fence : 0, lt,
+               lines};
+    const dim3 grid(static_cast<unsigned>(ceil_div(lines, lt) * a.blocksPerLine));
     const auto* tw2 = static_cast<const cx<T>*>(lp.tw2);
     if constexpr (decltype(eng)::kBatchedCopy) {
       auto k = long_rows_plain_kernel<decltype(eng), T, S>;
@@ -498,11 +520,27 @@ void bluestein_host_tables(int n, int m, std::vector<cx<T>>& chirp, std::vector<
 }
 }  // namespace
 
-bool needs_long_path(int n, bool dbl) {
+bool needs_long_path(int n, bool dbl, LongAxis axis) {
   if (n <= 1 || has_ct_kernel(n)) return false;
   if (n > max_device_fft_length(dbl)) return true;
-  if (largest_prime(n) <= kBluesteinPrime) return false;
-  return !use_bluestein(n, dbl ? sizeof(cx<double>) : sizeof(cx<float>));
+  const std::size_t eb = dbl ? sizeof(cx<double>) : sizeof(cx<float>);
+  if (largest_prime(n) > kBluesteinPrime && !use_bluestein(n, eb)) return true;
+  int lines = 0;
+  std::size_t lds = 0;
+  try {
+    lds = in_lds_engine_bytes(n, eb, lines);
+  } catch (const GPUFFTError&) {
+    return true;
+  }
+  std::size_t extra = 0;
+  if (axis == kLongAxisY) extra = static_cast<std::size_t>(n) * (sizeof(long long) + 2 * sizeof(int)) + 16;
+  if (axis == kLongAxisX) extra = static_cast<std::size_t>(n + 1) * sizeof(int) + 16 + lines * eb;
+  if (lds + extra > kLdsPerWorkgroup) return true;
+  if (axis != kLongAxisZ && static_cast<std::size_t>(lines) * eb < 64) {
+    for (int d = 16; d <= n / 16; d *= 2)
+      if (n % d == 0 && long_ct_factor(d) && long_ct_factor(n / d)) return true;
+  }
+  return false;
 }
 
 LongPlan long_plan(int n, bool dbl) {

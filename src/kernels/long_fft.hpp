@@ -1,19 +1,13 @@
 // Line FFTs that do not fit one workgroup's LDS (any length): a global-memory
 // four-step engine, and Bluestein's chirp-z convolution on top of it for
 // lengths whose large prime factor has no codelet. The fused stage kernels
-// handle every length up to the LDS capacity; an axis beyond it runs as
-// glue kernel (gather into natural-order lines) -> long FFT -> glue kernel
-// (scatter into the stage's output layout). Replaces the GPUFFTError of rounds
-// 1-2 (the reference's vendor plans take any n: src/fft/transform_1d_gpu.hpp:70,
+// handle every length up to the LDS capacity; a longer axis runs as two passes
+// whose loads and stores carry the stage's IO (LongIO in long_fft.hip: the
+// columns pass gathers from the stage source, the rows pass stores into the
+// stage destination). Replaces the GPUFFTError of rounds 1-2 (the reference's
+// vendor plans take any n: src/fft/transform_1d_gpu.hpp:70,
 // transform_2d_gpu.hpp:69).
 //
-// Four-step (n = n1 * n2, element j = j1 * n2 + j2 of a line):
-//   columns pass, in place: for every j2, FFT_n1 over j1 -> k1, times
-//     exp(S 2 pi i j2 k1 / n);
-//   rows pass, out of place: for every k1, FFT_n2 over j2 -> k2, stored at the
-//     natural position k1 + n1 * k2.
-// Both passes use the one-workgroup engines (compile-time, run-time or
-// Bluestein) on lines staged through LDS, with coalesced global walks.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -41,8 +35,17 @@ struct LongPlan {
   long long line_elems() const { return m > n ? m : n; }
 };
 
-// true if an axis of length n cannot run in the fused stage kernels
-bool needs_long_path(int n, bool dbl);
+// Whether an axis of length n runs the four-step path instead of the one-workgroup
+// stage kernels: lines that do not fit one workgroup's LDS next to the tables
+// the axis's stage kernels keep there (y: the column entries, x: the column
+// table and the C2R Nyquist line), and, on the line-fast y and x axes, run-time
+// engine lengths whose workgroup would hold lines of less than one 64-byte column
+// segment while n splits into two compile-time factors. Measured on MI355X,
+// 4096 x 64 x 64 C2C fp64: x stage in one-line workgroups 690 / 495 us
+// (forward / backward) against 383 / 308 us per 4096 elements on the four-step
+// at 8192 (profiles/r4/long/).
+enum LongAxis { kLongAxisZ = 0, kLongAxisY = 1, kLongAxisX = 2 };
+bool needs_long_path(int n, bool dbl, LongAxis axis);
 // plan (tables cached per device); throws GPUFFTError beyond 2^20 / 2
 LongPlan long_plan(int n, bool dbl);
 

@@ -1348,6 +1348,10 @@ struct BlueTables {
   const void* twm = nullptr;
 };
 bool use_bluestein(int n, std::size_t elemBytes);
+// LDS bytes and lines per workgroup of the one-workgroup engine (run-time or
+// Bluestein) of a length without a compile-time kernel; throws GPUFFTError when
+// a line does not fit
+std::size_t in_lds_engine_bytes(int n, std::size_t elemBytes, int& lines);
 BlueTables bluestein_tables(int n, bool dbl);
 
 template <class K>

@@ -218,6 +218,19 @@ BlueTables bluestein_tables(int n, bool dbl) {
   return t;
 }
 
+std::size_t in_lds_engine_bytes(int n, std::size_t elemBytes, int& lines) {
+  if (use_bluestein(n, elemBytes)) {
+    int m = 1;
+    while (m < 2 * n - 1) m *= 2;
+    lines = static_cast<int>(std::min<std::size_t>(
+        16, std::max<std::size_t>(1, kLdsBudget / (2 * static_cast<std::size_t>(m) * elemBytes))));
+    return 2 * static_cast<std::size_t>(lines) * m * elemBytes;
+  }
+  const RtPlan p = make_rt_plan(n, elemBytes);
+  lines = p.lines;
+  return static_cast<std::size_t>(p.inplace ? 1 : 2) * p.lines * p.ls * elemBytes;
+}
+
 int max_device_fft_length(bool dbl) { return (160 * 1024) / (2 * (dbl ? 16 : 8)) - 1; }
 
 bool has_ct_kernel(int n) {

@@ -1039,6 +1039,11 @@ def test_capped_intermediate_distributed(gpu, exchange, chunks, monkeypatch):
     ((4099, 3, 4), "c2c", True), ((3, 4099, 4), "c2c", True),
     ((12288, 4, 5), "r2c", False), ((4099, 4, 5), "r2c", False), ((6, 5, 6144), "r2c", False),
     ((4, 4099, 5), "r2c", False), ((24576, 3, 4), "r2c", True), ((4099, 3, 4), "r2c", True),
+    # fp32 8192 fits one workgroup's LDS as a line but not next to the x stage's column
+    # table; 4096 / 2048 on the line-fast axes take the four-step (one-line run-time
+    # workgroups); z at 4096 stays in LDS
+    ((8192, 3, 4), "c2c", True), ((4, 8192, 3), "c2c", True), ((4096, 4, 5), "c2c", False),
+    ((4, 2048, 5), "c2c", False), ((4096, 3, 4), "r2c", True), ((6, 4, 4096), "c2c", True),
 ])
 def test_long_lines_any_length(gpu, dims, ttype, single):
     import torch

@@ -169,12 +169,12 @@ def test_bench_driver_launch_2ranks_rccl(gpu, monkeypatch):
     assert r.returncode == 0, out[-4000:]
     rec = _bench_json(r.stdout)
     cfg = rec["config"]
-    assert cfg["data_plane"] == "rccl"
+    assert cfg["data_plane"] == "rccl" and cfg["exchange"] == "compact"
     chk = cfg["check_error"]
     assert chk["ranks_checked"] == 2 and chk["ok"] and chk["roundtrip"] < 1e-12
     for d in ("backward", "forward"):
         assert cfg["stage_ms"][d]["z"] > 0
-        assert cfg["exchange"]["ms"][d] > 0 and cfg["exchange"]["GBps_per_rank"][d] > 0
+        assert cfg["exchange_stats"]["ms"][d] > 0 and cfg["exchange_stats"]["GBps_per_rank"][d] > 0
     assert "64^3" in rec["metric"]
 
 
