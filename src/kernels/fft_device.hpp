@@ -229,6 +229,19 @@ struct ShapeMaxThreads<Sh, std::void_t<decltype(Sh::kMaxThr)>> {
 
 struct NoLoad {};  // input already placed in LDS at Engine::in_at(b, pos)
 
+// Element loads of the first pass. A load functor may also take the element's
+// offset from the lane's first position t (pos = t + off, off a compile-time
+// constant of the unrolled load): a kernel that addresses the lane's elements
+// from one base pointer then does no arithmetic on pos, which the compiler
+// cannot recover once it has turned t + off into t | off.
+template <class Load>
+__device__ __forceinline__ auto load_at(Load& load, int b, int t, int off) {
+  if constexpr (std::is_invocable<Load&, int, int, int>::value)
+    return load(b, t + off, off);
+  else
+    return load(b, t + off);
+}
+
 // largest power of two <= b, at most 16 (line-fast lane mapping)
 __host__ __device__ constexpr int lf_lines(int b) {
   int p = 1;
@@ -368,7 +381,7 @@ struct FftCT {
         if constexpr (std::is_same<Load, NoLoad>::value)
           v[k * Sh::R0 + r] = line[pad_index(j + r * (N / Sh::R0), PS)];
         else
-          v[k * Sh::R0 + r] = load(b, j + r * (N / Sh::R0));
+          v[k * Sh::R0 + r] = load_at(load, b, t, k * TP + r * (N / Sh::R0));
       }
     }
     compute<Sh::R0, 1>(v, t, tw);
@@ -578,7 +591,7 @@ struct FftMR {
         if constexpr (std::is_same<Load, NoLoad>::value)
           v[k * R + r] = line[pad_index(j + r * NB, PS)];
         else
-          v[k * R + r] = load(b, j + r * NB);
+          v[k * R + r] = load_at(load, b, t, k * TP + r * NB);
       }
     }
   }

@@ -426,11 +426,62 @@ __device__ __forceinline__ long long seg_index(const ZArgs& a, int s, int pos) {
 // Row side of a line-fast kernel: lanes walk along rows (row-contiguous global
 // loads) into the FFT lines in LDS; line-fast lanes would touch B rows with
 // (64/B)-element segments per wave instruction (32 B segments for fp32 B=16).
-template <class Eng, typename T, class Load>
-__device__ __forceinline__ void stage_rows(const Eng& eng, cx<T>* lds, int rows, int len, Load load) {
+// Row b of the tile starts at base + b * stride: complex elements, or real ones
+// (E == T) loaded with a zero imaginary part.
+template <typename E>
+struct RowSrc {
+  const E* base;
+  long long stride;
+};
+template <typename T, typename E>
+__device__ __forceinline__ cx<T> row_elem(const E* p) {
+  if constexpr (std::is_same<E, T>::value)
+    return mk<T>(ld_stream_real(p), T(0));
+  else
+    return ld_stream(p);
+}
+template <class Eng, typename T, typename E>
+__device__ __forceinline__ void stage_rows(const Eng& eng, cx<T>* lds, int rows, int len, RowSrc<E> src) {
+  if constexpr (!Eng::kBatchedCopy) {
+    // full tile of a compile-time engine: the trip count, and each unrolled
+    // load's row and position offsets, are compile-time (the row products are
+    // scalar), so the generic loop's per-element guards, divisions and 64-bit
+    // row multiplies go (fp32 y forward: 3 quarter-rate multiplies per load)
+    using F = typename Eng::F;
+    constexpr int N = Eng::kN, NT = F::NT, B = F::B;
+    constexpr int kIters = B * N / NT;
+    // (not the wide 512-thread engines: their kernels sit at the 128-VGPR
+    // occupancy step, fp32 512 y forward 127 -> 131 VGPRs and 241 -> 316 us with it)
+    if constexpr ((B * N) % NT == 0 && (NT % N == 0 || N % NT == 0) && kIters <= 32 &&
+                  NT <= kMaxThreads) {
+      if (rows == B) {
+        const int tid = static_cast<int>(threadIdx.x);
+        cx<T> v[kIters];
+        if constexpr (NT % N == 0) {
+          constexpr int RP = NT / N;  // rows per pass of the workgroup
+          const int b0 = tid / N, p = tid % N;
+          const E* p0 = src.base + static_cast<long long>(b0) * src.stride + p;
+#pragma unroll
+          for (int i = 0; i < kIters; ++i) v[i] = row_elem<T>(p0 + (i * RP) * src.stride);
+#pragma unroll
+          for (int i = 0; i < kIters; ++i) lds[eng.in_at(b0 + i * RP, p)] = v[i];
+        } else {
+          constexpr int C = N / NT;  // passes per row
+          const E* p0 = src.base + tid;
+#pragma unroll
+          for (int i = 0; i < kIters; ++i) v[i] = row_elem<T>(p0 + (i / C) * src.stride + (i % C) * NT);
+#pragma unroll
+          for (int i = 0; i < kIters; ++i) lds[eng.in_at(i / C, tid + (i % C) * NT)] = v[i];
+        }
+        __syncthreads();
+        return;
+      }
+    }
+  }
   gather_to_lds(lds, rows * len, [&](int idx) {
     const int b = idx / len;
-    return load(b, idx - b * len);
+    if (b >= rows) return czero<T>();
+    return row_elem<T>(src.base + static_cast<long long>(b) * src.stride + (idx - b * len));
   }, [&](int idx) {
     const int b = idx / len;
     return eng.in_at(b, idx - b * len);
@@ -804,12 +855,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     if (lb < nl) q = a.desc[s0 + lb];
     const int z0 = q.z0, len0 = lb < nl ? q.len0 : 0, z1 = q.z1, len1 = lb < nl ? q.count - q.len0 : 0;
     cx<T>* vals = values + q.valueStart;
-    eng.global_to_global(lds, tw, [&](int b, int pos) -> cx<T> {
-      // unconditional load (lanes past the last stick read a valid one): no
-      // branch per element, so the loads (and segment-table reads) issue back to back
-      const cx<T> v = cvt<T>(ld_stream(&in[seg.at(s0 + min(b, nl - 1), pos)]));
-      return b < nl ? v : czero<T>();
-    }, [&](int b, int pos, cx<T> v) {
+    auto store = [&](int b, int pos, cx<T> v) {
       assert(b == lb);
       // branch-free value offset (as in the backward kernel); one predicated store
       const unsigned j0 = static_cast<unsigned>(pos - z0), j1 = static_cast<unsigned>(pos - z1);
@@ -817,7 +863,23 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const bool in1 = j1 < static_cast<unsigned>(len1);
       const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
       if (in0 || in1) st_values(&vals[j], spfft::scale(v, scale));
-    });
+    };
+    // Lanes past the last stick load a valid stick (min(lb, nl - 1)) and store
+    // nothing (len0 = len1 = 0): no guard per element. Loads only the lane's own
+    // line (b == lb, the FftCT/FftMR contract).
+    const int ls = s0 + min(lb, nl - 1);
+    if (seg.single == 1) {
+      // plain stick rows (one rank): the row is the lane's base pointer, each
+      // element a constant offset from it; no segment-mode branch and no 64-bit
+      // multiply per element (the other modes below read a table per position)
+      const BT* row = in + static_cast<long long>(ls) * seg.stride + Eng::F::lane_pos();
+      eng.global_to_global(lds, tw, [&](int, int, int off) -> cx<T> { return cvt<T>(ld_stream(&row[off])); },
+                           store);
+    } else {
+      eng.global_to_global(lds, tw, [&](int, int pos) -> cx<T> {
+        return cvt<T>(ld_stream(&in[seg.at(ls, pos)]));
+      }, store);
+    }
   } else {
     StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
     for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -1063,10 +1125,8 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int zl = min(B, a.L - z0);
   constexpr bool kTable = y_table<Eng, has_store_pos<Eng>::value>();
   const ColEntries<Eng> ce(eng, a, lds, c, true, kTable);
-  auto load = [&](int b, int pos) -> cx<T> {
-    if (b >= zl) return czero<T>();
-    return ld_inter(&inter[static_cast<long long>(z0 + b) * a.interZStride + inter_row(a, c) + pos]);
-  };
+  const RowSrc<cx<T>> rows{inter + static_cast<long long>(z0) * a.interZStride + inter_row(a, c),
+                           a.interZStride};
   if constexpr (kTable) {
     // compile-time engines: the stick bases of the lane's output positions are
     // read from the y -> base table before the FFT (their LDS latency overlaps
@@ -1075,7 +1135,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     long long bases[F::kStoreSlots];
     F::for_each_store_pos([&](int i, int pos) { bases[i] = ce.yBase[pos]; });
     int slot = 0;
-    stage_rows(eng, lds, zl, n, load);
+    stage_rows(eng, lds, zl, n, rows);
     eng.lds_to_global(lds, tw, [&](int b, int, cx<T> v) {
       const long long base = bases[slot++];
       if (base >= 0 && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
@@ -1087,7 +1147,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     long long base;
     if (ce.find(pos, base) && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
   };
-  stage_rows(eng, lds, zl, n, load);
+  stage_rows(eng, lds, zl, n, rows);
   eng.lds_to_global(lds, tw, store);
   release_remote(a.remote);
 }
@@ -1182,12 +1242,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   build_xcol(a, xCol, n);
   const int yl = min(B, a.Y - y0);
   cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
-  auto load = [&](int b, int pos) -> cx<T> {
-    if (b >= yl) return czero<T>();
-    const long long row = (static_cast<long long>(zl) * a.Y + y0 + b) * n;
-    if (R2C) return mk<T>(ld_stream_real(&static_cast<const T*>(space)[row + pos]), T(0));
-    return ld_stream(&static_cast<const cx<T>*>(space)[row + pos]);
-  };
+  const long long row0 = (static_cast<long long>(zl) * a.Y + y0) * n;
   // arguments of the per-element stores pinned in scalar registers (see x_backward_kernel)
   const int rowStride = pin_uniform(static_cast<int>(a.interStride)), nFreq = pin_uniform(a.nFreq);
   const int dense = pin_uniform(x_dense(a) ? 1 : 0);
@@ -1195,7 +1250,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const int c = dense ? (pos < nFreq ? pos : -1) : xCol[pos];
     if (c >= 0 && b < yl) st_inter(&dst[c * rowStride + b], v);
   };
-  stage_rows(eng, lds, yl, n, load);
+  if constexpr (R2C)
+    stage_rows(eng, lds, yl, n, RowSrc<T>{static_cast<const T*>(space) + row0, n});
+  else
+    stage_rows(eng, lds, yl, n, RowSrc<cx<T>>{static_cast<const cx<T>*>(space) + row0, n});
   eng.lds_to_global(lds, tw, store);
 }
 
@@ -1319,7 +1377,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     // first pass loads the real rows straight from global memory
     eng.global_to_lds(lds, twh, rowLoad);
   } else {
-    stage_rows(eng, lds, yl, h, rowLoad);
+    stage_rows(eng, lds, yl, h, RowSrc<cx<T>>{row0, h});
     eng.lds_to_lds(lds, twh);
   }
   cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
