@@ -171,7 +171,7 @@ void GpuExecutor<T>::log_plan() const {
   const bool dbl = sizeof(T) == 8;
   auto describe = [&](bool isLong, const dev::LongPlan& lp, int n, bool lf) -> std::string {
     if (!isLong) return dev::describe_engine(n, dbl, lf);
-    return "long n=" + std::to_string(n) + (lp.bluestein ? " bluestein m=" + std::to_string(lp.m) : "") +
+    return "long n=" + std::to_string(lp.n) + (lp.bluestein ? " bluestein m=" + std::to_string(lp.m) : "") +
            " four-step " + std::to_string(lp.n1) + "x" + std::to_string(lp.n2);
   };
   std::string plane = "none";
