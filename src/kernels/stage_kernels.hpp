@@ -1,4 +1,4 @@
-// Device code of the fused stage kernels (included by z/y/x_stage.hip).
+// Device code of the fused stage kernels (included by stage_launch.hpp and long_fft.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -1373,7 +1373,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     return b >= yl ? czero<T>() : ld_stream(row0 + static_cast<long long>(b) * h + m);
   };
   if constexpr (!Eng::kBatchedCopy && !Eng::kLineFast) {
-    // row-mapped engine (x_stage_fwd.hip): a line's lanes are adjacent, so the
+    // row-mapped engine (launch_x_forward): a line's lanes are adjacent, so the
     // first pass loads the real rows straight from global memory
     eng.global_to_lds(lds, twh, rowLoad);
   } else {

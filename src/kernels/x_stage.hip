@@ -1,49 +1,23 @@
-// x-stage launchers: [z][column][y] <-> space domain rows (C2C, C2R, R2C).
+// x-stage kernels, fp64 transforms, and the host helpers of the stage engines
+// (run-time plans, Bluestein tables, engine descriptions).
 #include <string>
 #include <vector>
 #include <tuple>
 #include <mutex>
 #include <map>
 
-#include "kernels/stage_kernels.hpp"
+#include "kernels/stage_launch.hpp"
 
 // after the HIP headers (codelets use __forceinline__ under hipcc)
 #include "fft/host_fft.hpp"
 
-
 namespace spfft {
 namespace dev {
 
-template <typename T>
-void launch_x_backward(const XArgs& a, bool r2c, const cx<T>* inter, void* space,
-                       const cx<T>* tw, const cx<T>* twHalf, hipStream_t stream) {
-  if (a.L <= a.zBegin || a.Y <= 0) return;
-  if (r2c && twHalf && a.n % 2 == 0 && a.n >= 4) {
-    with_engine<T, +1, true>(a.n / 2, [&](auto eng, int threads, int lines, std::size_t lds) {
-      auto k = x_backward_c2r_kernel<decltype(eng), T>;
-      const std::size_t ldsTotal =
-          lds + std::size_t(lines) * sizeof(cx<T>) + std::size_t(a.n / 2 + 1) * sizeof(int) + 16;
-      prepare_kernel(k, ldsTotal);
-      hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal,
-                         stream, eng, a, inter, static_cast<T*>(space), twHalf, tw);
-      gpu_check_launch("x_backward_c2r", stream);
-    });
-    return;
-  }
-  with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
-    auto k = r2c ? x_backward_kernel<decltype(eng), T, true> : x_backward_kernel<decltype(eng), T, false>;
-    const std::size_t ldsTotal = lds + std::size_t(a.n) * sizeof(int) + 16;
-    prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.Y, lines), a.L - a.zBegin, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
-                       inter, space, tw);
-    gpu_check_launch("x_backward", stream);
-  });
-}
-
-template void launch_x_backward<double>(const XArgs&, bool, const cx<double>*, void*,
-                                        const cx<double>*, const cx<double>*, hipStream_t);
-template void launch_x_backward<float>(const XArgs&, bool, const cx<float>*, void*,
-                                       const cx<float>*, const cx<float>*, hipStream_t);
+template void launch_x_backward<double>(const XArgs&, bool, const cx<double>*, void*, const cx<double>*,
+                                     const cx<double>*, hipStream_t);
+template void launch_x_forward<double>(const XArgs&, bool, const void*, cx<double>*, const cx<double>*,
+                                    const cx<double>*, hipStream_t);
 
 // ------------------------------------------------------------------ helpers
 namespace {

@@ -1,0 +1,13 @@
+// z-stage kernels, fp64 transforms with fp32 exchange buffers (*_FLOAT exchanges).
+#include "kernels/stage_launch.hpp"
+
+namespace spfft {
+namespace dev {
+
+template void launch_z_backward<double, cx<float>>(const ZArgs&, const cx<double>*, cx<float>*, const cx<double>*,
+                                             hipStream_t);
+template void launch_z_forward<double, cx<float>>(const ZArgs&, const cx<float>*, cx<double>*, double, const cx<double>*,
+                                            hipStream_t);
+
+}  // namespace dev
+}  // namespace spfft
