@@ -942,12 +942,17 @@ template <class Eng, class = void>
 struct has_store_pos : std::false_type {};
 template <class Eng>
 struct has_store_pos<Eng, std::void_t<decltype(Eng::F::kStoreSlots)>> : std::true_type {};
+// "No stick entry" in the y -> base tables. Bases are element offsets from the
+// stage's buffer, and the peer-write plane's are offsets to the peers' buffers,
+// which lie below the local one as often as above: -1 would be a valid base.
+constexpr long long kNoBase = -(1LL << 62);
+
 template <class Eng>
 struct ColEntries {
   bool useDesc;
   ColDesc d;
   long long stride;
-  long long* yBase;  // LDS: y -> stick-side base or -1 (table mode)
+  long long* yBase;  // LDS: y -> stick-side base or kNoBase (table mode)
   long long* cBase;  // LDS: colBase per entry (list mode)
   int* yEnt;         // LDS: y -> entry or -1 (list mode)
   int* cY;           // LDS: entry -> y (list mode)
@@ -972,7 +977,7 @@ struct ColEntries {
       if (table) {
         for (int y = threadIdx.x; y < n; y += blockDim.x) {
           long long b;
-          yBase[y] = col_desc_find(d, stride, y, b) ? b : -1;
+          yBase[y] = col_desc_find(d, stride, y, b) ? b : kNoBase;
         }
         __syncthreads();
       }
@@ -981,7 +986,7 @@ struct ColEntries {
     const int k0 = a.colOffsets[c];
     ne = a.colOffsets[c + 1] - k0;
     if (table) {
-      for (int y = threadIdx.x; y < n; y += blockDim.x) yBase[y] = -1;
+      for (int y = threadIdx.x; y < n; y += blockDim.x) yBase[y] = kNoBase;
       __syncthreads();
       for (int e = threadIdx.x; e < ne; e += blockDim.x) yBase[a.colY[k0 + e]] = a.colBase[k0 + e];
       __syncthreads();
@@ -1062,7 +1067,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   auto load = [&](int b, int pos) -> cx<T> {
     if constexpr (kTable) {
       const long long base = ce.yBase[pos];
-      const BT* p = (base >= 0 && b < zl) ? in + (base + z0 + b) : zsrc;
+      const BT* p = (base != kNoBase && b < zl) ? in + (base + z0 + b) : zsrc;
       return cvt<T>(ld_stream(p));
     } else {
       long long base;
@@ -1138,7 +1143,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     stage_rows(eng, lds, zl, n, rows);
     eng.lds_to_global(lds, tw, [&](int b, int, cx<T> v) {
       const long long base = bases[slot++];
-      if (base >= 0 && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+      if (base != kNoBase && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
     });
     release_remote(a.remote);
     return;

@@ -551,6 +551,50 @@ def test_gpu_virtual_ranks_distributions(gpu, dist, chunks, exchange, blocks, mo
         assert e < tol
 
 
+@pytest.mark.parametrize("dims,sticks,planes", [
+    ((2, 64, 5), [1, 1], [1, 1]), ((2, 64, 5), [1, 1], [0, 1]), ((2, 64, 5), [1, 0], [0, 1]),
+    ((4, 32, 6), [1, 2, 1], [1, 0, 2]), ((3, 128, 4), [0, 1, 1], [1, 1, 0])])
+def test_unbuffered_skewed_distributions(gpu, dims, sticks, planes):
+    """UNBUFFERED (peer writes) with y lengths on the compile-time engines, whose y stage
+    reads the stick bases from an LDS table: a peer's buffer below the local one gives a
+    negative base, which the table's old -1 "no entry" marker dropped (found by
+    tools/fuzz_gpu.py). Every rank with planes writes into every rank with sticks."""
+    import torch
+    from spfft_amd.parallel import run_ranks
+    from spfft_amd.utils.indices import calculate_num_local_xy_planes
+    nx, ny, nz = dims
+    P = len(sticks)
+    rng = np.random.default_rng(64)
+    parts = create_value_indices(rng, sticks, 0.9, 0.8, nx, ny, nz, False)
+    pl = [calculate_num_local_xy_planes(r, nz, planes) for r in range(P)]
+    offsets = np.concatenate([[0], np.cumsum(pl)])
+    all_idx = np.concatenate(parts)
+    field = rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))
+    vals = dense_forward(field, all_idx, dims)
+    ref = dense_backward(all_idx, vals, dims)
+    starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
+    ms = max(len(np.unique(p[:, 0].astype(np.int64) * ny + p[:, 1])) if len(p) else 0 for p in parts)
+
+    def body(rank, comm):
+        torch.cuda.set_device(0)
+        grid = sp.Grid(nx, ny, nz, max(1, ms), GPU, 1, max_local_z_length=max(pl), comm=comm,
+                       exchange_type=sp.ExchangeType.UNBUFFERED)
+        t = grid.create_transform(GPU, sp.TransformType.C2C, nx, ny, nz, pl[rank], parts[rank])
+        errs = []
+        for _ in range(2):
+            v = torch.as_tensor(vals[starts[rank]:starts[rank + 1]], device="cuda")
+            out = t.backward(v).cpu().numpy()
+            errs.append(max_rel_error(out, ref[offsets[rank]:offsets[rank + 1]]) if pl[rank] else 0.0)
+            slab = torch.as_tensor(np.ascontiguousarray(field[offsets[rank]:offsets[rank + 1]]),
+                                   device="cuda")
+            f = t.forward(slab).cpu().numpy()
+            errs.append(max_rel_error(f, vals[starts[rank]:starts[rank + 1]]) if len(f) else 0.0)
+        return max(errs)
+
+    for e in run_ranks(P, body):
+        assert e < 1e-11
+
+
 @pytest.mark.parametrize("dims,ttype", [((16, 12, 20), "c2c"), ((11, 13, 12), "c2c"),
                                         ((16, 10, 14), "r2c"), ((15, 8, 9), "r2c"),
                                         ((64, 64, 64), "c2c")])
