@@ -55,6 +55,12 @@ def run_case(rng, case, max_elems):
     if sum(plane_dist) == 0:
         plane_dist[-1] = 1.0
     parts = create_value_indices(rng, stick_dist, fill, float(rng.uniform(0.4, 1.0)), nx, ny, nz, r2c)
+    centred = bool(rng.random() < 0.3)
+    if centred:  # the same index set in centred form (negative frequencies)
+        half = np.array([nx // 2, ny // 2, nz // 2])
+        n3 = np.array([nx, ny, nz])
+        parts = [np.where(p > half, p - n3, p).astype(np.int32) for p in parts]
+    multi = P == 1 and bool(rng.random() < 0.25)
     planes = [calculate_num_local_xy_planes(r, nz, plane_dist) for r in range(P)]
     offsets = np.concatenate([[0], np.cumsum(planes)])
     all_idx = np.concatenate(parts)
@@ -69,7 +75,8 @@ def run_case(rng, case, max_elems):
     rdt = torch.float32 if single else torch.float64
     tol = 2e-4 if (single or exchange.endswith("FLOAT")) else 1e-10
     desc = (f"case {case}: dims={dims} {'R2C' if r2c else 'C2C'} {'fp32' if single else 'fp64'} P={P} "
-            f"{exchange if P > 1 else 'local'} sticks={stick_dist} planes={plane_dist}")
+            f"{exchange if P > 1 else 'local'} sticks={stick_dist} planes={plane_dist}"
+            f"{' centred' if centred else ''}{' multi_transform x3' if multi else ''}")
 
     def body(rank, comm):
         torch.cuda.set_device(0)
@@ -88,7 +95,25 @@ def run_case(rng, case, max_elems):
         ef = max_rel_error(f, vals[starts[rank]:starts[rank + 1]]) if len(f) else 0.0
         return max(e, ef)
 
-    errs = [body(0, None)] if P == 1 else run_ranks(P, body)
+    def multi_body():
+        # three transforms of the same problem on their own grids, one multi_transform call
+        ts = []
+        for _ in range(3):
+            grid = G(nx, ny, nz, nx * ny, sp.ProcessingUnit.GPU, 1)
+            ts.append((grid, grid.create_transform(sp.ProcessingUnit.GPU, ttype, nx, ny, nz, nz, parts[0])))
+        v = torch.as_tensor(vals, dtype=cdt, device="cuda")
+        outs = sp.multi_transform_backward([t for _, t in ts], [v] * 3)
+        e = max(max_rel_error(o.cpu().numpy(), ref) for o in outs)
+        sl = torch.as_tensor(np.ascontiguousarray(field), dtype=rdt if r2c else cdt, device="cuda")
+        for _, t in ts:  # forward input: each transform's own space domain
+            t.space_domain(sp.ProcessingUnit.GPU).copy_(sl.reshape(t.space_domain(sp.ProcessingUnit.GPU).shape))
+        fs = sp.multi_transform_forward([t for _, t in ts])
+        return max(e, max(max_rel_error(f.cpu().numpy(), vals) for f in fs))
+
+    if multi:
+        errs = [multi_body()]
+    else:
+        errs = [body(0, None)] if P == 1 else run_ranks(P, body)
     return desc, max(errs), tol
 
 
