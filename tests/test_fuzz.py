@@ -1,0 +1,37 @@
+"""Randomised sweeps of tools/fuzz_gpu.py inside the suites: every engine path, type,
+precision, 1-3 ranks with random distributions, every exchange type, centred indices
+and multi_transform batches, against the dense numpy oracle."""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fuzz():
+    spec = importlib.util.spec_from_file_location("fuzz_gpu", os.path.join(REPO, "tools", "fuzz_gpu.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _sweep(host, cases, seed, max_elems):
+    mod = _fuzz()
+    rng = np.random.default_rng(seed)
+    bad = []
+    for c in range(cases):
+        desc, err, tol = mod.run_case(rng, c, max_elems, host=host)
+        if not err < tol:
+            bad.append(f"{desc} err={err:.2e}")
+    assert not bad, "\n".join(bad)
+
+
+def test_fuzz_host():
+    _sweep(True, 40, 2024, 1 << 17)
+
+
+@pytest.mark.gpu
+def test_fuzz_gpu(gpu):
+    _sweep(False, 150, 2025, 1 << 20)

@@ -35,7 +35,7 @@ def draw_dims(rng, max_elems):
             return tuple(dims)
 
 
-def run_case(rng, case, max_elems):
+def run_case(rng, case, max_elems, host=False):
     import torch
     import spfft_amd as sp
     from spfft_amd.parallel import run_ranks
@@ -70,6 +70,18 @@ def run_case(rng, case, max_elems):
     ref = dense_backward(all_idx, vals, dims, r2c=r2c)
     starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
     ttype = sp.TransformType.R2C if r2c else sp.TransformType.C2C
+    PU = sp.ProcessingUnit.HOST if host else sp.ProcessingUnit.GPU
+    nthreads = 2 if host else 1
+
+    def dev(x, complex_):
+        """Input array for the processing unit (numpy on the host, a GPU tensor)."""
+        if host:
+            return np.ascontiguousarray(x, dtype=(np.complex64 if single else np.complex128) if complex_
+                                        else (np.float32 if single else np.float64))
+        return torch.as_tensor(x, dtype=(cdt if complex_ else rdt), device="cuda")
+
+    def npy(y):
+        return y if host else y.cpu().numpy()
     G = sp.GridFloat if single else sp.Grid
     cdt = torch.complex64 if single else torch.complex128
     rdt = torch.float32 if single else torch.float64
@@ -79,19 +91,20 @@ def run_case(rng, case, max_elems):
             f"{' centred' if centred else ''}{' multi_transform x3' if multi else ''}")
 
     def body(rank, comm):
-        torch.cuda.set_device(0)
+        if not host:
+            torch.cuda.set_device(0)
         if P == 1:
-            grid = G(nx, ny, nz, nx * ny, sp.ProcessingUnit.GPU, 1)
+            grid = G(nx, ny, nz, nx * ny, PU, nthreads)
         else:
             ms = max(len(np.unique(p[:, 0].astype(np.int64) * ny + p[:, 1])) if len(p) else 0 for p in parts)
-            grid = G(nx, ny, nz, max(1, ms), sp.ProcessingUnit.GPU, 1, max_local_z_length=max(planes),
+            grid = G(nx, ny, nz, max(1, ms), PU, nthreads, max_local_z_length=max(planes),
                      comm=comm, exchange_type=getattr(sp.ExchangeType, exchange))
-        t = grid.create_transform(sp.ProcessingUnit.GPU, ttype, nx, ny, nz, planes[rank], parts[rank])
-        v = torch.as_tensor(vals[starts[rank]:starts[rank + 1]], dtype=cdt, device="cuda")
-        out = t.backward(v).cpu().numpy()
+        t = grid.create_transform(PU, ttype, nx, ny, nz, planes[rank], parts[rank])
+        v = dev(vals[starts[rank]:starts[rank + 1]], True)
+        out = npy(t.backward(v))
         e = max_rel_error(out, ref[offsets[rank]:offsets[rank + 1]]) if planes[rank] else 0.0
         slab = np.ascontiguousarray(field[offsets[rank]:offsets[rank + 1]])
-        f = t.forward(torch.as_tensor(slab, dtype=rdt if r2c else cdt, device="cuda")).cpu().numpy()
+        f = npy(t.forward(dev(slab, not r2c)))
         ef = max_rel_error(f, vals[starts[rank]:starts[rank + 1]]) if len(f) else 0.0
         return max(e, ef)
 
@@ -99,16 +112,20 @@ def run_case(rng, case, max_elems):
         # three transforms of the same problem on their own grids, one multi_transform call
         ts = []
         for _ in range(3):
-            grid = G(nx, ny, nz, nx * ny, sp.ProcessingUnit.GPU, 1)
-            ts.append((grid, grid.create_transform(sp.ProcessingUnit.GPU, ttype, nx, ny, nz, nz, parts[0])))
-        v = torch.as_tensor(vals, dtype=cdt, device="cuda")
+            grid = G(nx, ny, nz, nx * ny, PU, nthreads)
+            ts.append((grid, grid.create_transform(PU, ttype, nx, ny, nz, nz, parts[0])))
+        v = dev(vals, True)
         outs = sp.multi_transform_backward([t for _, t in ts], [v] * 3)
-        e = max(max_rel_error(o.cpu().numpy(), ref) for o in outs)
-        sl = torch.as_tensor(np.ascontiguousarray(field), dtype=rdt if r2c else cdt, device="cuda")
+        e = max(max_rel_error(npy(o), ref) for o in outs)
+        sl = dev(np.ascontiguousarray(field), not r2c)
         for _, t in ts:  # forward input: each transform's own space domain
-            t.space_domain(sp.ProcessingUnit.GPU).copy_(sl.reshape(t.space_domain(sp.ProcessingUnit.GPU).shape))
+            d = t.space_domain(PU)
+            if host:
+                d[...] = sl.reshape(d.shape)
+            else:
+                d.copy_(sl.reshape(d.shape))
         fs = sp.multi_transform_forward([t for _, t in ts])
-        return max(e, max(max_rel_error(f.cpu().numpy(), vals) for f in fs))
+        return max(e, max(max_rel_error(npy(f), vals) for f in fs))
 
     if multi:
         errs = [multi_body()]
@@ -122,13 +139,15 @@ def main():
     ap.add_argument("--cases", type=int, default=100)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-elems", type=int, default=1 << 20)
+    ap.add_argument("--pu", choices=["gpu", "host"], default="gpu",
+                    help="host: the same sweep on SPFFT_PU_HOST (runs without a GPU)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     bad = 0
     t0 = time.time()
     for c in range(a.cases):
         try:
-            desc, err, tol = run_case(rng, c, a.max_elems)
+            desc, err, tol = run_case(rng, c, a.max_elems, host=a.pu == "host")
         except Exception as e:  # a refused or failing case is reported, not fatal
             desc, err, tol = f"case {c}: {type(e).__name__}: {e}", float("inf"), 0.0
         ok = err < tol
