@@ -35,3 +35,29 @@ def test_fuzz_host():
 @pytest.mark.gpu
 def test_fuzz_gpu(gpu):
     _sweep(False, 150, 2025, 1 << 20)
+
+
+def _launch_dist(nproc, *args, env_extra=None):
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={nproc}", os.path.join(REPO, "tools", "fuzz_dist.py"), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "passed" in out and "FAIL" not in out, out[-4000:]
+
+
+def test_fuzz_dist_host_3ranks():
+    """The random cases on three OS processes over torch.distributed (host engine)."""
+    _launch_dist(3, "--host", "--cases", "20", "--seed", "31", "--max-elems", "65536")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plane", ["ipc", "rccl"])
+def test_fuzz_dist_gpu_3ranks(gpu, plane):
+    """The random cases on three processes sharing the GPU: the IPC peer-write plane, or
+    one multi-rank RCCL communicator (SPFFT_RCCL_VIRTUAL_HOSTS=1)."""
+    extra = {"SPFFT_RCCL_VIRTUAL_HOSTS": "1"} if plane == "rccl" else {}
+    _launch_dist(3, "--cases", "25", "--seed", "32", "--max-elems", "262144", env_extra=extra)
