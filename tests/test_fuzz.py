@@ -52,12 +52,3 @@ def _launch_dist(nproc, *args, env_extra=None):
 def test_fuzz_dist_host_3ranks():
     """The random cases on three OS processes over torch.distributed (host engine)."""
     _launch_dist(3, "--host", "--cases", "20", "--seed", "31", "--max-elems", "65536")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("plane", ["ipc", "rccl"])
-def test_fuzz_dist_gpu_3ranks(gpu, plane):
-    """The random cases on three processes sharing the GPU: the IPC peer-write plane, or
-    one multi-rank RCCL communicator (SPFFT_RCCL_VIRTUAL_HOSTS=1)."""
-    extra = {"SPFFT_RCCL_VIRTUAL_HOSTS": "1"} if plane == "rccl" else {}
-    _launch_dist(3, "--cases", "25", "--seed", "32", "--max-elems", "262144", env_extra=extra)
