@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-elems", type=int, default=1 << 19)
     ap.add_argument("--host", action="store_true")
+    ap.add_argument("--only", type=int, default=-1, help="run only this case (the draws of the others still happen)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -76,8 +77,11 @@ def main():
         starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
         ms = max(len(np.unique(p[:, 0].astype(np.int64) * ny + p[:, 1])) if len(p) else 0 for p in parts)
         tol = 2e-4 if (single or exchange.endswith("FLOAT")) else 1e-10
+        if a.only >= 0 and c != a.only:
+            continue
         err = 0.0
         msg = ""
+        eb = ef = 0.0
         try:
             G = sp.GridFloat if single else sp.Grid
             grid = G(nx, ny, nz, max(1, ms), PU, 1, max_local_z_length=max(planes), comm=TorchDistComm(),
@@ -92,10 +96,14 @@ def main():
                 v, slab = torch.as_tensor(v, device="cuda"), torch.as_tensor(slab, device="cuda")
             out = t.backward(v)
             out = out if a.host else out.cpu().numpy()
-            err = max_rel_error(out, ref[offsets[rank]:offsets[rank + 1]]) if planes[rank] else 0.0
+            eb = max_rel_error(out, ref[offsets[rank]:offsets[rank + 1]]) if planes[rank] else 0.0
             f = t.forward(slab)
             f = f if a.host else f.cpu().numpy()
-            err = max(err, max_rel_error(f, vals[starts[rank]:starts[rank + 1]]) if len(f) else 0.0)
+            ef = max_rel_error(f, vals[starts[rank]:starts[rank + 1]]) if len(f) else 0.0
+            err = max(eb, ef)
+            if a.only >= 0:
+                print(f"rank {rank}: values={len(parts[rank])} planes={planes[rank]} backward={eb:.2e} "
+                      f"forward={ef:.2e}", flush=True)
             plane = grid.data_plane if not a.host else "host"
         except Exception as e:  # reported, and agreed on below
             err, msg, plane = float("inf"), f"{type(e).__name__}: {e}", "?"
