@@ -10,6 +10,7 @@ SPFFT_RCCL_VIRTUAL_HOSTS=1.
         tools/fuzz_dist.py --cases 50 [--host]
 """
 import argparse
+import gc
 import importlib.util
 import os
 import sys
@@ -34,6 +35,8 @@ def main():
     ap.add_argument("--max-elems", type=int, default=1 << 19)
     ap.add_argument("--host", action="store_true")
     ap.add_argument("--only", type=int, default=-1, help="run only this case (the draws of the others still happen)")
+    ap.add_argument("--teardown", choices=["lazy", "collective"], default="lazy",
+                    help="collective: drop each case's grid on every rank, then barrier, before the next case")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -50,7 +53,12 @@ def main():
     PU = sp.ProcessingUnit.HOST if a.host else sp.ProcessingUnit.GPU
     rng = np.random.default_rng(a.seed)  # the same draws on every rank
     bad = 0
+    grid = t = None
     for c in range(a.cases):
+        if a.teardown == "collective":
+            grid = t = None
+            gc.collect()
+            dist.barrier()
         nx, ny, nz = dims = fz.draw_dims(rng, a.max_elems)
         r2c = bool(rng.random() < 0.4)
         single = bool(rng.random() < 0.4)
