@@ -546,6 +546,7 @@ public:
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     if (flags_) (void)hipFree(flags_);
     if (failHost_) (void)hipHostFree(failHost_);
+    if (fenceEv_) (void)hipEventDestroy(fenceEv_);
   }
 
   void exchange(const void*, void*, const std::vector<Transfer>&, hipStream_t,
@@ -592,6 +593,12 @@ private:
     if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) == kAborted) check();
     DeviceGuard guard(device_);
     if (ipc_) {
+      if (sysFence_) {
+        // experiment (SPFFT_PEER_SYSFENCE=1): a system-scope release of every
+        // XCD's L2 ahead of the barrier kernel, whose own fences act on one XCD
+        if (!fenceEv_) gpu_check(hipEventCreate(&fenceEv_), "hipEventCreate");
+        gpu_check(hipEventRecord(fenceEv_, stream), "hipEventRecord");
+      }
       dev::launch_peer_barrier(table_->data<unsigned long long*>(),
                                static_cast<unsigned long long*>(flags_), me_, P_, ++epoch_,
                                failDev_, timeoutTicks_, stream);
@@ -617,6 +624,11 @@ private:
   unsigned long long epoch_ = 0;
   long long timeoutTicks_ = 0;
   bool readPending_[2] = {false, false};
+  bool sysFence_ = [] {
+    const char* e = std::getenv("SPFFT_PEER_SYSFENCE");
+    return e && *e == '1';
+  }();
+  hipEvent_t fenceEv_ = nullptr;
 };
 
 struct NodeInfo {
