@@ -141,7 +141,7 @@ GridImpl<T>::~GridImpl() {
     // release device resources on the grid's device
     try {
       DeviceGuard guard(deviceId_);
-      devComm_.reset();
+      devComm_.reset();  // (returns leased exchange sides to the IPC arena)
       for (auto& d : dev_) d.reset();
     } catch (...) {
     }
@@ -169,7 +169,7 @@ std::size_t GridImpl<T>::device_bytes() const {
   std::size_t b = 0;
   for (const auto& d : dev_)
     if (d) b += d->bytes();
-  return b;
+  return b + sideOverrideBytes_[0] + sideOverrideBytes_[1];
 }
 
 template <typename T>
@@ -187,6 +187,7 @@ template <typename T>
 void* GridImpl<T>::device_slot(Slot s) {
   if (!(pu_ & SPFFT_PU_GPU)) throw InvalidParameterError();
   if (s == kSlabSide && local()) s = kStickSide;
+  if (s <= kSlabSide && sideOverride_[s]) return sideOverride_[s];
   return dev_[s]->data();
 }
 
@@ -196,7 +197,18 @@ DeviceComm& GridImpl<T>::device_comm() {
   if (!devComm_) {
     void* const buffers[2] = {dev_[kStickSide] ? dev_[kStickSide]->data() : nullptr,
                               dev_[kSlabSide] ? dev_[kSlabSide]->data() : nullptr};
-    devComm_ = DeviceComm::create(comm_, deviceId_, exchange_, buffers);
+    const std::size_t bytes[2] = {dev_[kStickSide] ? dev_[kStickSide]->bytes() : 0,
+                                  dev_[kSlabSide] ? dev_[kSlabSide]->bytes() : 0};
+    devComm_ = DeviceComm::create(comm_, deviceId_, exchange_, buffers, bytes);
+    // a data plane that owns the exchange sides (cross-process peer writes:
+    // memory leased from the IPC arena) replaces the grid's own allocations
+    for (int s = 0; s < 2; ++s) {
+      if (void* p = devComm_->local_buffer(s)) {
+        sideOverride_[s] = p;
+        sideOverrideBytes_[s] = dev_[s] ? dev_[s]->bytes() : 0;
+        dev_[s].reset();
+      }
+    }
   }
   return *devComm_;
 }

@@ -108,6 +108,9 @@ private:
   HostBuffer host_[kNumSlots];
   std::unique_ptr<DeviceBuffer> dev_[kNumSlots];
   std::unique_ptr<DeviceComm> devComm_;
+  // exchange sides owned by the data plane (DeviceComm::local_buffer)
+  void* sideOverride_[2] = {nullptr, nullptr};
+  std::size_t sideOverrideBytes_[2] = {0, 0};
   std::mutex allocMutex_;
   std::mutex execMutex_;
 };

@@ -19,6 +19,7 @@
 #include "core/common.hpp"
 #include "core/timing.hpp"
 #include "gpu/gpu_runtime.hpp"
+#include "gpu/ipc_arena.hpp"
 #include "kernels/peer_sync.hpp"
 #include "spfft/exceptions.hpp"
 
@@ -456,65 +457,104 @@ private:
 };
 
 // ------------------------------------------------------------- peer writes
+// The ordered stream of a process's peer barriers: one per member set and
+// device (the key of the RCCL channels, so the same ordering-domain rules
+// apply), shared by every grid and transform of the process that talks to the
+// same ranks. Each barrier round is handed over from the caller's stream with
+// an event, runs on this stream, and hands back with a second event, so
+//  - barrier kernels of one process run one at a time in host call order, the
+//    order every rank issues them in (transforms are collective): epochs are
+//    published in increasing order even when the transforms of one grid run
+//    on different streams, and no spinning barrier sits in a user stream's
+//    hardware queue in front of work it waits for;
+//  - the hand-off events are system-scope releases: the CP writes back every
+//    XCD's L2 (the stage kernels' peer stores included) before the barrier
+//    publishes the epoch. A fence inside the one-workgroup barrier kernel acts
+//    on one XCD only.
+struct PeerChannel {
+  int device = 0;
+  std::unique_ptr<GpuStream> stream;
+  hipEvent_t in = nullptr, out = nullptr;
+  std::mutex m;
+
+  explicit PeerChannel(int dev) : device(dev) {
+    DeviceGuard guard(device);
+    stream.reset(new GpuStream(true));
+    const unsigned flags = hipEventDisableTiming | hipEventReleaseToSystem;
+    gpu_check(hipEventCreateWithFlags(&in, flags), "hipEventCreateWithFlags");
+    gpu_check(hipEventCreateWithFlags(&out, flags), "hipEventCreateWithFlags");
+  }
+  ~PeerChannel() {
+    if (process_exiting()) return;
+    if (in) (void)hipEventDestroy(in);
+    if (out) (void)hipEventDestroy(out);
+  }
+};
+
+std::mutex gPeerChannelMutex;
+std::map<std::string, std::weak_ptr<PeerChannel>>& peer_channel_registry() {
+  static auto* r = new std::map<std::string, std::weak_ptr<PeerChannel>>();  // outlives atexit
+  return *r;
+}
+
+std::shared_ptr<PeerChannel> acquire_peer_channel(const std::string& key, int device) {
+  std::lock_guard<std::mutex> lock(gPeerChannelMutex);
+  auto& reg = peer_channel_registry();
+  auto it = reg.find(key);
+  std::shared_ptr<PeerChannel> ch = it != reg.end() ? it->second.lock() : nullptr;
+  if (!ch) {
+    ch = std::make_shared<PeerChannel>(device);
+    reg[key] = ch;
+  }
+  return ch;
+}
+
+// SPFFT_PEER_BARRIER=host: cross-process barrier rounds on the host (stream
+// synchronise + communicator barrier) instead of barrier kernels; the default
+// "device" keeps the exchange stream-ordered.
+bool peer_barrier_on_host() {
+  static const bool host = [] {
+    const char* e = std::getenv("SPFFT_PEER_BARRIER");
+    return e && std::string(e) == "host";
+  }();
+  return host;
+}
+
 class PeerDeviceComm : public DeviceComm {
 public:
+  // In-process group (ipc == false): `buffers` are the grid's exchange sides,
+  // shared by plain pointers. Across processes (ipc == true) the exchange
+  // sides and the flag array are leased from the IPC arena (ipc_arena.hpp)
+  // and the grid switches to them (local_buffer); `bytes` are the sides'
+  // sizes.
   PeerDeviceComm(const std::shared_ptr<Communicator>& comm, int device, void* const buffers[2],
-                 bool ipc)
+                 const std::size_t bytes[2], bool ipc, const std::string& channelKey)
       : comm_(comm), device_(device), me_(comm->rank()), P_(comm->size()), ipc_(ipc) {
     DeviceGuard guard(device);
-    const std::size_t fbytes = ((static_cast<std::size_t>(std::max(P_, 1)) * 8 + 4095) / 4096) * 4096;
-    // flags are polled by the barrier kernel: uncached so remote stores are seen
-    if (hipExtMallocWithFlags(&flags_, fbytes, hipDeviceMallocUncached) != hipSuccess) {
-      (void)hipGetLastError();
-      gpu_check(hipMalloc(&flags_, fbytes), "hipMalloc");
-    }
-    gpu_check(hipMemset(flags_, 0, fbytes), "hipMemset");
     gpu_check(hipHostMalloc(reinterpret_cast<void**>(&failHost_), 64,
                             hipHostMallocMapped | hipHostMallocCoherent),
               "hipHostMalloc");
     *failHost_ = 0;
     gpu_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev_), failHost_, 0),
               "hipHostGetDevicePointer");
-
-    void* local[3] = {buffers[0], buffers[1], flags_};
     peers_.assign(P_, {nullptr, nullptr, nullptr});
+    const std::size_t fbytes = static_cast<std::size_t>(std::max(P_, 1)) * 16;
     if (ipc_) {
-      struct Exported {
-        hipIpcMemHandle_t h[3];
-        int valid[3];
-      };
-      Exported mine;
-      std::memset(&mine, 0, sizeof(mine));
-      for (int i = 0; i < 3; ++i) {
-        if (!local[i]) continue;
-        gpu_check(hipIpcGetMemHandle(&mine.h[i], local[i]), "hipIpcGetMemHandle");
-        mine.valid[i] = 1;
-      }
-      std::vector<Exported> all(P_);
-      comm_->allgather(&mine, all.data(), sizeof(Exported));
-      for (int q = 0; q < P_; ++q) {
-        for (int i = 0; i < 3; ++i) {
-          if (q == me_) {
-            peers_[q][i] = local[i];
-          } else if (all[q].valid[i]) {
-            void* p = nullptr;
-            gpu_check(hipIpcOpenMemHandle(&p, all[q].h[i], hipIpcMemLazyEnablePeerAccess),
-                      "hipIpcOpenMemHandle");
-            opened_.push_back(p);
-            peers_[q][i] = p;
-          }
-        }
-      }
+      open_ipc(bytes, fbytes);
+      if (!peer_barrier_on_host()) channel_ = acquire_peer_channel(channelKey, device);
     } else {
+      // in-process groups meet on the host: ranks of one process share its few
+      // hardware queues, so a spinning barrier kernel could sit in front of
+      // the very work it waits for
       struct Raw {
-        void* p[3];
+        void* p[2];
         int device;
       };
-      Raw mine{{local[0], local[1], local[2]}, device};
+      Raw mine{{buffers[0], buffers[1]}, device};
       std::vector<Raw> all(P_);
       comm_->allgather(&mine, all.data(), sizeof(Raw));
       for (int q = 0; q < P_; ++q) {
-        for (int i = 0; i < 3; ++i) peers_[q][i] = all[q].p[i];
+        for (int i = 0; i < 2; ++i) peers_[q][i] = all[q].p[i];
         if (all[q].device != device) {
           const hipError_t e = hipDeviceEnablePeerAccess(all[q].device, 0);
           if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) gpu_check(e, "hipDeviceEnablePeerAccess");
@@ -522,14 +562,6 @@ public:
         }
       }
     }
-    std::vector<unsigned long long*> table(P_);
-    for (int q = 0; q < P_; ++q) {
-      table[q] = static_cast<unsigned long long*>(peers_[q][2]);
-      if (!table[q]) throw InternalError();
-    }
-    table_.reset(new DeviceBuffer(sizeof(void*) * P_));
-    gpu_check(hipMemcpy(table_->data(), table.data(), sizeof(void*) * P_, hipMemcpyHostToDevice),
-              "hipMemcpy");
     int rateKHz = 0;
     gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, device),
               "hipDeviceGetAttribute");
@@ -542,11 +574,19 @@ public:
 
   ~PeerDeviceComm() override {
     if (process_exiting()) return;
-    DeviceGuard guard(device_);
-    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
-    if (flags_) (void)hipFree(flags_);
-    if (failHost_) (void)hipHostFree(failHost_);
-    if (fenceEv_) (void)hipEventDestroy(fenceEv_);
+    try {
+      DeviceGuard guard(device_);
+      // the last barrier round of this plane has finished before its flag
+      // array goes back to the arena (the caller's streams were synchronised
+      // by the executors; the channel stream may still hold the round)
+      if (channel_) (void)hipStreamSynchronize(channel_->stream->get());
+      for (void* p : opened_) ipc_close(p);
+      // a plane that saw a failure may still receive a late peer's marks:
+      // its flag array is not reused
+      if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) != 0 && flags_) flags_->discard();
+      if (failHost_) (void)hipHostFree(failHost_);
+    } catch (...) {
+    }
   }
 
   void exchange(const void*, void*, const std::vector<Transfer>&, hipStream_t,
@@ -558,6 +598,10 @@ public:
   bool host_synchronous() const override { return false; }
   bool peer_writes() const override { return true; }
   void* peer_buffer(int rank, int slot) const override { return peers_.at(rank).at(slot); }
+  void* local_buffer(int slot) const override {
+    if (!ipc_ || slot < 0 || slot > 1 || !sides_[slot]) return nullptr;
+    return sides_[slot]->data();
+  }
   void prepare_write(int slot, hipStream_t stream) override {
     if (readPending_[slot & 1]) barrier(stream);
   }
@@ -573,39 +617,130 @@ public:
   bool healthy(std::string* detail) override {
     const unsigned f = __atomic_load_n(failHost_, __ATOMIC_ACQUIRE);
     if (f == 0) return true;
-    if (detail)
-      *detail = f == kAborted ? "peer exchange: aborted (host-side timeout or an earlier failure)"
-                              : "peer exchange: a rank did not reach the exchange barrier in time";
+    if (detail) {
+      if (f & kAborted)
+        *detail = "peer exchange: aborted (host-side timeout or an earlier failure)";
+      else if (f & kTimedOut)
+        *detail = "peer exchange: a rank did not reach the exchange barrier within SPFFT_PEER_TIMEOUT";
+      else if (f & kPeerGaveUp)
+        *detail = "peer exchange: a peer rank gave up waiting at the exchange barrier";
+      else
+        *detail = "peer exchange: failure word " + std::to_string(f);
+    }
     return false;
   }
   void abort() override {
     // the barrier kernels poll this word and stop waiting
-    unsigned expected = 0;
-    __atomic_compare_exchange_n(failHost_, &expected, kAborted, false, __ATOMIC_ACQ_REL,
-                                __ATOMIC_ACQUIRE);
+    __atomic_fetch_or(failHost_, kAborted, __ATOMIC_ACQ_REL);
   }
   const char* kind() const override { return ipc_ ? "ipc" : "peer"; }
+  std::string describe() const override {
+    if (!ipc_) return kind();
+    const IpcArenaStats s = ipc_arena_stats();
+    char b[160];
+    std::snprintf(b, sizeof(b), "ipc (%d ranks, barrier on %s; arena: %lld blocks allocated, %lld reused, %lld freed)",
+                  P_, channel_ ? "peer channel" : "host", s.allocated, s.reused, s.freed);
+    return b;
+  }
 
 private:
-  static constexpr unsigned kAborted = 2;
+  static constexpr unsigned kTimedOut = 1, kAborted = 2, kPeerGaveUp = 4;
+
+  // Leases the two exchange sides and the flag array, announces them
+  // (handles + headers) and maps every peer's, checking each mapping's header
+  // against the announcement. Every rank learns every rank's outcome before
+  // anyone throws, so no rank is left in a later collective.
+  void open_ipc(const std::size_t bytes[2], std::size_t fbytes) {
+    struct Announce {
+      IpcExport e[3];
+    };
+    struct Outcome {
+      int ok;
+      char why[200];
+    };
+    Announce mine{};
+    Outcome res{1, {0}};
+    try {
+      for (int i = 0; i < 2; ++i)
+        if (bytes[i] > 0) sides_[i] = ipc_acquire(device_, bytes[i], false);
+      flags_ = ipc_acquire(device_, fbytes, true);
+      gpu_check(hipMemset(flags_->data(), 0, fbytes), "hipMemset");
+      for (int i = 0; i < 2; ++i)
+        if (sides_[i]) mine.e[i] = sides_[i]->describe();
+      mine.e[2] = flags_->describe();
+      // fault injection (SPFFT_FAULT_IPC_NONCE=1): the last rank announces a
+      // nonce its flag array does not carry, as a stale mapping would show
+      const char* fi = std::getenv("SPFFT_FAULT_IPC_NONCE");
+      if (fi && *fi == '1' && me_ == P_ - 1) mine.e[2].header.nonce ^= 1;
+    } catch (const std::exception& ex) {
+      res.ok = 0;
+      std::snprintf(res.why, sizeof(res.why), "IPC arena: %s", ex.what());
+    }
+    std::vector<Announce> all(P_);
+    comm_->allgather(&mine, all.data(), sizeof(Announce));
+    if (res.ok) {
+      try {
+        for (int q = 0; q < P_ && res.ok; ++q) {
+          for (int i = 0; i < 3 && res.ok; ++i) {
+            if (q == me_) {
+              peers_[q][i] = i < 2 ? (sides_[i] ? sides_[i]->data() : nullptr) : flags_->data();
+              continue;
+            }
+            if (!all[q].e[i].valid) {
+              if (i == 2) {
+                res.ok = 0;
+                std::snprintf(res.why, sizeof(res.why), "rank %d announced no flag array", q);
+              }
+              continue;
+            }
+            std::string why;
+            void* p = ipc_open_checked(all[q].e[i], &why);
+            if (!p) {
+              res.ok = 0;
+              std::snprintf(res.why, sizeof(res.why), "rank %d <- rank %d: %s", me_, q, why.c_str());
+              break;
+            }
+            opened_.push_back(p);
+            peers_[q][i] = p;
+          }
+        }
+      } catch (const std::exception& ex) {
+        res.ok = 0;
+        std::snprintf(res.why, sizeof(res.why), "hipIpcOpenMemHandle: %s %s", ex.what(),
+                      error_detail().c_str());
+      }
+    }
+    std::vector<Outcome> outs(P_);
+    comm_->allgather(&res, outs.data(), sizeof(Outcome));
+    for (const Outcome& o : outs) {
+      if (o.ok) continue;
+      for (void* p : opened_) ipc_close(p);
+      opened_.clear();
+      set_error_detail(std::string("peer exchange setup: ") + o.why);
+      throw MPIError();
+    }
+    std::vector<unsigned long long*> table(P_);
+    for (int q = 0; q < P_; ++q) table[q] = static_cast<unsigned long long*>(peers_[q][2]);
+    table_.reset(new DeviceBuffer(sizeof(void*) * P_));
+    gpu_check(hipMemcpy(table_->data(), table.data(), sizeof(void*) * P_, hipMemcpyHostToDevice),
+              "hipMemcpy");
+  }
+
   void barrier(hipStream_t stream) {
     SPFFT_TIMED_SCOPE("peer_barrier");
-    if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) == kAborted) check();
+    if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) != 0) check();
     DeviceGuard guard(device_);
-    if (ipc_) {
-      if (sysFence_) {
-        // experiment (SPFFT_PEER_SYSFENCE=1): a system-scope release of every
-        // XCD's L2 ahead of the barrier kernel, whose own fences act on one XCD
-        if (!fenceEv_) gpu_check(hipEventCreate(&fenceEv_), "hipEventCreate");
-        gpu_check(hipEventRecord(fenceEv_, stream), "hipEventRecord");
-      }
+    if (channel_) {
+      std::lock_guard<std::mutex> lock(channel_->m);
+      hipStream_t cs = channel_->stream->get();
+      gpu_check(hipEventRecord(channel_->in, stream), "hipEventRecord");
+      gpu_check(hipStreamWaitEvent(cs, channel_->in, 0), "hipStreamWaitEvent");
       dev::launch_peer_barrier(table_->data<unsigned long long*>(),
-                               static_cast<unsigned long long*>(flags_), me_, P_, ++epoch_,
-                               failDev_, timeoutTicks_, stream);
+                               static_cast<unsigned long long*>(flags_->data()), me_, P_, ++epoch_,
+                               failDev_, timeoutTicks_, cs);
+      gpu_check(hipEventRecord(channel_->out, cs), "hipEventRecord");
+      gpu_check(hipStreamWaitEvent(stream, channel_->out, 0), "hipStreamWaitEvent");
     } else {
-      // ranks of one process share its few hardware queues: a spinning barrier
-      // kernel could sit in front of the very work it waits for, so in-process
-      // groups meet on the host instead
       gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
       comm_->barrier();
     }
@@ -615,20 +750,17 @@ private:
   std::shared_ptr<Communicator> comm_;
   int device_, me_, P_;
   bool ipc_;
-  void* flags_ = nullptr;
   unsigned int* failHost_ = nullptr;
   unsigned int* failDev_ = nullptr;
+  std::unique_ptr<IpcLease> sides_[2];
+  std::unique_ptr<IpcLease> flags_;
   std::vector<std::array<void*, 3>> peers_;
   std::vector<void*> opened_;
   std::unique_ptr<DeviceBuffer> table_;
+  std::shared_ptr<PeerChannel> channel_;
   unsigned long long epoch_ = 0;
   long long timeoutTicks_ = 0;
   bool readPending_[2] = {false, false};
-  bool sysFence_ = [] {
-    const char* e = std::getenv("SPFFT_PEER_SYSFENCE");
-    return e && *e == '1';
-  }();
-  hipEvent_t fenceEv_ = nullptr;
 };
 
 struct NodeInfo {
@@ -705,7 +837,7 @@ int DeviceComm::rccl_channels_created() { return gChannelsCreated.load(); }
 
 std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicator>& comm,
                                                int device, SpfftExchangeType exchange,
-                                               void* const buffers[2]) {
+                                               void* const buffers[2], const std::size_t bytes[2]) {
   if (!comm) throw InternalError();
   const bool unbuffered = exchange == SPFFT_EXCH_UNBUFFERED;
   const int prefLocal = env_choice("SPFFT_GPU_EXCHANGE");
@@ -723,7 +855,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
       }
       return std::unique_ptr<DeviceComm>(new RcclSelfDeviceComm(comm, ch));
     }
-    if (unbuffered) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, false));
+    if (unbuffered) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, false, std::string()));
     return std::unique_ptr<DeviceComm>(new LoopbackDeviceComm(comm));
   }
   // SPFFT_RCCL_VIRTUAL_HOSTS=1 (rehearsals on a box with fewer GPUs than
@@ -734,11 +866,18 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   // send/receive order, grouped calls, channel stream hand-offs.
   const char* vh = std::getenv("SPFFT_RCCL_VIRTUAL_HOSTS");
   const bool virtualHosts = vh && *vh == '1';
+  // Rehearsal mode only. The host id is set once per process, before this
+  // process's first RCCL initialisation, and is keyed on the process (not on
+  // its rank in whichever communicator comes first), so every communicator
+  // the process joins later sees the same host.
   if (virtualHosts) {
-    const std::string id = "spfft-virtual-host-" + std::to_string(comm->rank());
-    setenv("NCCL_HOSTID", id.c_str(), 1);
-    setenv("NCCL_IB_DISABLE", "1", 0);
-    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    static std::once_flag once;
+    std::call_once(once, [] {
+      const std::string id = "spfft-virtual-host-" + std::to_string(static_cast<long long>(getpid()));
+      setenv("NCCL_HOSTID", id.c_str(), 1);
+      setenv("NCCL_IB_DISABLE", "1", 0);
+      setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    });
   }
   // data-plane choice, identical on every rank (decided from allgathered facts)
   NodeInfo mine{};
@@ -774,7 +913,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   const int fault = all[0].fault;
   const bool peer =
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
-  if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, true));
+  if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
   auto ch = acquire_channel(comm.get(), key, device, comm->rank(), P, false, fault);
   // every rank learns whether every RCCL communicator came up
   int ok = ch->ok() ? 1 : 0;
@@ -794,7 +933,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   }
   if (comm->rank() == 0)
     std::fprintf(stderr, "spfft: %s; using the peer-write (IPC) data plane\n", why.c_str());
-  return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, true));
+  return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
 }
 
 }  // namespace spfft

@@ -78,9 +78,10 @@ struct ExchangeSync {
 class DeviceComm {
 public:
   // Collective. `buffers` are the grid's two exchange slots (0 = stick side,
-  // 1 = slab side; base pointers of device allocations).
+  // 1 = slab side; base pointers of device allocations of `bytes` bytes).
   static std::unique_ptr<DeviceComm> create(const std::shared_ptr<Communicator>& comm, int device,
-                                            SpfftExchangeType exchange, void* const buffers[2]);
+                                            SpfftExchangeType exchange, void* const buffers[2],
+                                            const std::size_t bytes[2]);
   virtual ~DeviceComm();
 
   // Runs a transfer list (collective: every rank calls with its own list).
@@ -116,6 +117,11 @@ public:
   virtual void prepare_write(int /*slot*/, hipStream_t /*stream*/) {}
   virtual void complete_writes(hipStream_t /*stream*/) {}
   virtual void note_read(int /*slot*/) {}
+  // Exchange side `slot` (0 stick side, 1 slab side) owned by the data plane,
+  // which the grid uses instead of its own allocation (the cross-process peer
+  // plane leases exported memory from the IPC arena); null if the grid's own
+  // buffer is used.
+  virtual void* local_buffer(int /*slot*/) const { return nullptr; }
   // Throws if an asynchronous failure (e.g. a barrier timeout) was recorded.
   virtual void check() {}
   // Failure detection while the host waits on a stream that carries exchanges:

@@ -52,3 +52,11 @@ def _launch_dist(nproc, *args, env_extra=None):
 def test_fuzz_dist_host_3ranks():
     """The random cases on three OS processes over torch.distributed (host engine)."""
     _launch_dist(3, "--host", "--cases", "20", "--seed", "31", "--max-elems", "65536")
+
+
+@pytest.mark.gpu
+def test_fuzz_dist_gpu_ipc_lazy_teardown(gpu):
+    """Three processes sharing the GPU over the IPC peer-write plane, grids dropped
+    lazily (each rank's previous grid lives until the next one exists). This is the
+    sweep that failed in round 4 (seed 8: wrong results at cases 27/29, then a hang)."""
+    _launch_dist(3, "--cases", "40", "--seed", "8")

@@ -222,3 +222,34 @@ def test_exchange_failure_detected(gpu, mode):
     seconds = float(line[0].split()[1])
     assert seconds < 5.0, line[0]
     assert ("SPFFT_COMM_TIMEOUT" in line[0]) if mode == "host-timeout" else ("barrier" in line[0])
+
+
+def _launch_tool(nproc, tool, *args, env_extra=None, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={nproc}", os.path.join(REPO, "tools", tool), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    return r.returncode, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_ipc_grid_churn_uneven_teardown(gpu):
+    """Grids created collectively and destroyed by the ranks at different times
+    (one rank drops its grid at once, the others keep it past the next grid's
+    creation), two transforms per grid on different streams, empty sides, every
+    exchange type, ending with a fresh UNBUFFERED grid. Destroying a grid must need
+    no peer (reference: src/memory/gpu_array.hpp:88)."""
+    code, out = _launch_tool(3, "ipc_churn.py", "--rounds", "14")
+    assert code == 0, out[-4000:]
+    assert "14/14 rounds passed" in out and "plane=ipc" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_ipc_stale_mapping_detected(gpu, monkeypatch):
+    """A mapping whose header does not carry the owner's announced nonce (fault
+    injection: the last rank announces a wrong one) is reported as MPIError on
+    every rank at grid setup; nothing is computed on it."""
+    code, out = _launch_tool(2, "rccl_probe.py", "UNBUFFERED",
+                             env_extra={"SPFFT_FAULT_IPC_NONCE": "1"}, timeout=180)
+    assert code != 0, out[-4000:]
+    assert out.count("stale IPC mapping") >= 2, out[-4000:]
