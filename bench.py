@@ -31,9 +31,37 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # transforms/s of the reference's vendor-FFT calls alone on one MI355X, 256^3
-# C2C fp64 r = N/2 (tools/ref_pipeline_bench.py), by the
-# number of transforms per step (T on T streams)
+# C2C fp64 r = N/2 (tools/ref_pipeline_bench.py), by
+# the number of transforms per step (T on T streams)
 REF_FFT_ONLY_256_BY_T = {1: 2210.2, 4: 2418.3}  # profiles/r3/comparator/
+
+# xGMI bandwidth one peer pair gets per direction (one link of an MI355X node:
+# 153.6 GB/s per link both directions, ~70 GB/s usable one way), the model's
+# assumption until the driver's N = 2/4/8 runs measure it
+LINK_GBPS = 70.0
+
+
+def _model(stages, sent_per_rank, world, chunks, blocks):
+    """Modelled per-direction times of a distributed step (README, "Multi-GPU
+    scaling"): every rank sends sent/(N-1) bytes to each peer over its own link, all
+    links at once, so the exchange takes link_ms = sent/(N-1) / LINK_GBPS; the
+    compute is this run's own z and y/x stage times. The pipelined grid of K plane
+    chunks x I stick blocks overlaps all but one step's compute with the link:
+    predicted = max(link, compute) + compute / (K * I) (unpipelined: link + compute).
+    The driver's measured ms_per_step / (2 T) can be read against `predicted_ms`."""
+    per_peer = sent_per_rank / max(1, world - 1)
+    link_ms = per_peer / (LINK_GBPS * 1e9) * 1e3
+    out = {"link_GBps_assumed": LINK_GBPS, "bytes_per_peer": per_peer,
+           "chunks": chunks, "stick_blocks": blocks}
+    for d in ("backward", "forward"):
+        st = stages.get(d, {})
+        compute = sum(v for k, v in st.items() if k not in ("exchange", "exchange-span", "exchange-tail", "total"))
+        steps = max(1, chunks * blocks)
+        pred = (max(link_ms, compute) + compute / steps) if steps > 1 else (link_ms + compute)
+        out[d] = {"link_ms": link_ms, "compute_ms": compute, "predicted_ms": pred,
+                  "bound": "link" if link_ms > compute else "compute"}
+    out["predicted_pair_ms"] = out["backward"]["predicted_ms"] + out["forward"]["predicted_ms"]
+    return out
 
 
 def parse():
@@ -297,6 +325,12 @@ def main():
         e = torch.tensor([float(sent)], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         exch["max_bytes_sent_per_rank"] = float(e.item())
+    model = None
+    if world > 1 and stages:
+        chunks, blocks, peer_writes = t.exchange_plan()
+        model = _model(stages, exch["max_bytes_sent_per_rank"], world, chunks, blocks)
+        model["peer_writes"] = peer_writes
+        model["shared_device"] = min(world, ndev) < world
     # ranks that share a device (rehearsal on a small box) are not a multi-GPU
     # measurement: record how many distinct devices the job really used
     n_devices = min(world, ndev)
@@ -349,6 +383,7 @@ def main():
                 "stage_ms_basis": (f"transform 0 alone, median of {a.profile_reps} backward+forward "
                                    "pairs after the timed loop (hipEvent stage marks)" if stages else None),
                 "exchange_stats": exch,
+                "model_ms": model,
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),
             },

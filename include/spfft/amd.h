@@ -75,6 +75,15 @@ SPFFT_EXPORT SpfftError spfft_amd_rccl_communicators(int* count);
  * on a transform's first call unless it was given a stream before) and RCCL
  * channel streams (one per shared communicator). */
 SPFFT_EXPORT SpfftError spfft_amd_library_streams(int* count);
+/* Exchange plan of a GPU transform: plane chunks K and stick blocks I of the
+ * pipelined all-to-all (1 and 1: one exchange per direction), and whether the
+ * stage kernels write into the peers directly (UNBUFFERED / IPC plane). Host
+ * transforms report 0, 0, 0. */
+SPFFT_EXPORT SpfftError spfft_amd_transform_exchange_plan(SpfftTransform transform, int* chunks,
+                                                          int* stickBlocks, int* peerWrites);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_exchange_plan(SpfftFloatTransform transform,
+                                                                int* chunks, int* stickBlocks,
+                                                                int* peerWrites);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 

@@ -72,7 +72,6 @@ def _check_targets():
 # change makes a kernel spill. Round 2 found such a regression by profiling: a
 # second FFT call site put 188 B of scratch into the run-time-engine y stage.
 # The report lists VGPRs / scratch of every kernel in build/kernel_resources.txt.
-_SPILL_EXEMPT = ("fused",)  # opt-in persistent experiment (profiles/README.md)
 
 
 def _check_kernel_resources(objs):
@@ -103,7 +102,7 @@ def _check_kernel_resources(objs):
             # spills and real scratch traffic are not
             spills = (int(meta.get("vgpr_spill_count", "0")) > 0 or
                       int(meta.get("private_segment_fixed_size", "0")) > 64)
-            if spills and not any(x in name for x in _SPILL_EXEMPT):
+            if spills:
                 bad.append(rows[-1])
 
         for line in notes.splitlines():

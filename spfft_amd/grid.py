@@ -355,6 +355,13 @@ class _TransformBase:
     def synchronize(self):
         _check(self._prec.amd_fn("transform_synchronize")(self._h))
 
+    def exchange_plan(self):
+        """(plane chunks K, stick blocks I, peer writes) of the GPU exchange pipeline."""
+        k, i, pw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(self._prec.amd_fn("transform_exchange_plan")(self._h, ctypes.byref(k), ctypes.byref(i),
+                                                            ctypes.byref(pw)))
+        return k.value, i.value, bool(pw.value)
+
     def rank_z_range(self, rank: int):
         off, ln = ctypes.c_int(), ctypes.c_int()
         _check(lib().spfft_amd_transform_local_z_offset_rank(self._h, rank, ctypes.byref(off),

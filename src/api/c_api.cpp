@@ -11,6 +11,7 @@
 #include "core/common.hpp"
 #include "core/timing.hpp"
 #include "gpu/device_comm.hpp"
+#include "gpu/gpu_executor.hpp"
 #include "spfft/amd.h"
 #include "spfft/exceptions.hpp"
 #include "spfft/grid.hpp"
@@ -141,6 +142,16 @@ template <class Impl>
 const char* data_plane_of(Impl& impl) {
   if (!(impl.processing_unit() & SPFFT_PU_GPU) || impl.local()) return "none";
   return impl.device_comm().kind();
+}
+}  // namespace
+
+namespace {
+template <typename T, class X>
+void exchange_plan_of(X& x, int* chunks, int* stickBlocks, int* peerWrites) {
+  auto* g = x.impl()->gpu();
+  *chunks = g ? g->exchange_chunks() : 0;
+  *stickBlocks = g ? g->exchange_stick_blocks() : 0;
+  *peerWrites = g && g->exchange_peer_writes() ? 1 : 0;
 }
 }  // namespace
 
@@ -384,6 +395,19 @@ SpfftError spfft_amd_library_streams(int* count) {
   if (!count) return SPFFT_INVALID_PARAMETER_ERROR;
   *count = spfft::GpuStream::live();
   return SPFFT_SUCCESS;
+}
+
+SpfftError spfft_amd_transform_exchange_plan(SpfftTransform t, int* chunks, int* stickBlocks,
+                                             int* peerWrites) {
+  if (!chunks || !stickBlocks || !peerWrites) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<Transform>(
+      t, [&](Transform& x) { exchange_plan_of<double>(x, chunks, stickBlocks, peerWrites); });
+}
+SpfftError spfft_amd_float_transform_exchange_plan(SpfftFloatTransform t, int* chunks,
+                                                   int* stickBlocks, int* peerWrites) {
+  if (!chunks || !stickBlocks || !peerWrites) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<TransformFloat>(
+      t, [&](TransformFloat& x) { exchange_plan_of<float>(x, chunks, stickBlocks, peerWrites); });
 }
 
 SpfftError spfft_amd_transform_set_stream(SpfftTransform t, void* stream, int synchronous) {

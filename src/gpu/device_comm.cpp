@@ -161,8 +161,12 @@ struct NcclChannel {
   // A failed call leaves the communicator (and an open group) in an undefined
   // state: the channel is aborted before the error propagates, so later
   // exchanges on it fail fast instead of reusing it. Caller holds `m`.
+  // Per-exchange calls wait under SPFFT_COMM_TIMEOUT (default 0 = no limit, a
+  // slow peer is not an error; asynchronous errors still end the wait): the
+  // channel is shared by every grid of the process, and a deadline here would
+  // abort all of them for one late peer.
   void nccl_check(ncclResult_t r, const char* what) {
-    if (r == ncclInProgress) r = settle(r, comm_init_timeout_seconds());
+    if (r == ncclInProgress) r = settle(r, comm_timeout_seconds());
     if (r != ncclSuccess) {
       set_error_detail(std::string("RCCL ") + what + ": " +
                        (r == ncclInProgress ? std::string("no progress") : ncclGetErrorString(r)) + " " +
@@ -457,20 +461,35 @@ private:
 };
 
 // ------------------------------------------------------------- peer writes
-// The ordered stream of a process's peer barriers: one per member set and
-// device (the key of the RCCL channels, so the same ordering-domain rules
-// apply), shared by every grid and transform of the process that talks to the
-// same ranks. Each barrier round is handed over from the caller's stream with
-// an event, runs on this stream, and hands back with a second event, so
-//  - barrier kernels of one process run one at a time in host call order, the
-//    order every rank issues them in (transforms are collective): epochs are
-//    published in increasing order even when the transforms of one grid run
-//    on different streams, and no spinning barrier sits in a user stream's
-//    hardware queue in front of work it waits for;
-//  - the hand-off events are system-scope releases: the CP writes back every
-//    XCD's L2 (the stage kernels' peer stores included) before the barrier
-//    publishes the epoch. A fence inside the one-workgroup barrier kernel acts
-//    on one XCD only.
+// Where the barrier rounds of the cross-process peer plane run
+// (SPFFT_PEER_BARRIER, documented in docs/USER_GUIDE.md):
+//  - "stream" (default): the barrier kernel on the caller's stream, right
+//    behind the stage kernel it frames. The rounds of one plane stay in issue
+//    order when transforms of one grid run on different streams: a round
+//    issued on another stream than the previous round first waits for that
+//    round (an event), so epochs are never published out of order;
+//  - "channel": every round of the process on one ordered stream per member
+//    set (PeerChannel), handed over by events. Costs two event hops per round:
+//    +52 us per round against "host" at 128^3 on 2 ranks sharing a GPU
+//    (profiles/r5/ipc);
+//  - "host": stream synchronise + communicator barrier, as in-process groups.
+enum class PeerBarrier { kStream, kChannel, kHost };
+PeerBarrier peer_barrier_mode() {
+  static const PeerBarrier m = [] {
+    const char* e = std::getenv("SPFFT_PEER_BARRIER");
+    const std::string v = e ? e : "";
+    return v == "host" ? PeerBarrier::kHost : (v == "channel" ? PeerBarrier::kChannel : PeerBarrier::kStream);
+  }();
+  return m;
+}
+
+// The ordered stream of a process's peer barriers in "channel" mode: one per
+// member set and device (the key of the RCCL channels, so the same
+// ordering-domain rules apply), shared by every grid and transform of the
+// process that talks to the same ranks. Each round is handed over from the
+// caller's stream with an event, runs on this stream, and hands back with a
+// second event, so the rounds of one process run one at a time in host call
+// order, the order every rank issues them in (transforms are collective).
 struct PeerChannel {
   int device = 0;
   std::unique_ptr<GpuStream> stream;
@@ -480,9 +499,8 @@ struct PeerChannel {
   explicit PeerChannel(int dev) : device(dev) {
     DeviceGuard guard(device);
     stream.reset(new GpuStream(true));
-    const unsigned flags = hipEventDisableTiming | hipEventReleaseToSystem;
-    gpu_check(hipEventCreateWithFlags(&in, flags), "hipEventCreateWithFlags");
-    gpu_check(hipEventCreateWithFlags(&out, flags), "hipEventCreateWithFlags");
+    gpu_check(hipEventCreateWithFlags(&in, hipEventDisableTiming), "hipEventCreateWithFlags");
+    gpu_check(hipEventCreateWithFlags(&out, hipEventDisableTiming), "hipEventCreateWithFlags");
   }
   ~PeerChannel() {
     if (process_exiting()) return;
@@ -509,17 +527,6 @@ std::shared_ptr<PeerChannel> acquire_peer_channel(const std::string& key, int de
   return ch;
 }
 
-// SPFFT_PEER_BARRIER=host: cross-process barrier rounds on the host (stream
-// synchronise + communicator barrier) instead of barrier kernels; the default
-// "device" keeps the exchange stream-ordered.
-bool peer_barrier_on_host() {
-  static const bool host = [] {
-    const char* e = std::getenv("SPFFT_PEER_BARRIER");
-    return e && std::string(e) == "host";
-  }();
-  return host;
-}
-
 class PeerDeviceComm : public DeviceComm {
 public:
   // In-process group (ipc == false): `buffers` are the grid's exchange sides,
@@ -538,10 +545,13 @@ public:
     gpu_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev_), failHost_, 0),
               "hipHostGetDevicePointer");
     peers_.assign(P_, {nullptr, nullptr, nullptr});
-    const std::size_t fbytes = static_cast<std::size_t>(std::max(P_, 1)) * 16;
+    const std::size_t fbytes = static_cast<std::size_t>(dev::peer_flag_words(std::max(P_, 1))) * 8;
     if (ipc_) {
       open_ipc(bytes, fbytes);
-      if (!peer_barrier_on_host()) channel_ = acquire_peer_channel(channelKey, device);
+      mode_ = peer_barrier_mode();
+      if (mode_ == PeerBarrier::kChannel) channel_ = acquire_peer_channel(channelKey, device);
+      if (mode_ == PeerBarrier::kStream)
+        gpu_check(hipEventCreateWithFlags(&orderEv_, hipEventDisableTiming), "hipEventCreateWithFlags");
     } else {
       // in-process groups meet on the host: ranks of one process share its few
       // hardware queues, so a spinning barrier kernel could sit in front of
@@ -580,6 +590,10 @@ public:
       // array goes back to the arena (the caller's streams were synchronised
       // by the executors; the channel stream may still hold the round)
       if (channel_) (void)hipStreamSynchronize(channel_->stream->get());
+      if (orderEv_) {
+        (void)hipEventSynchronize(orderEv_);
+        (void)hipEventDestroy(orderEv_);
+      }
       for (void* p : opened_) ipc_close(p);
       // a plane that saw a failure may still receive a late peer's marks:
       // its flag array is not reused
@@ -638,8 +652,10 @@ public:
     if (!ipc_) return kind();
     const IpcArenaStats s = ipc_arena_stats();
     char b[160];
+    const char* where = mode_ == PeerBarrier::kStream ? "caller stream"
+                        : mode_ == PeerBarrier::kChannel ? "peer channel" : "host";
     std::snprintf(b, sizeof(b), "ipc (%d ranks, barrier on %s; arena: %lld blocks allocated, %lld reused, %lld freed)",
-                  P_, channel_ ? "peer channel" : "host", s.allocated, s.reused, s.freed);
+                  P_, where, s.allocated, s.reused, s.freed);
     return b;
   }
 
@@ -730,16 +746,23 @@ private:
     SPFFT_TIMED_SCOPE("peer_barrier");
     if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) != 0) check();
     DeviceGuard guard(device_);
-    if (channel_) {
+    unsigned long long* const* table = table_ ? table_->data<unsigned long long*>() : nullptr;
+    unsigned long long* mine = flags_ ? static_cast<unsigned long long*>(flags_->data()) : nullptr;
+    if (mode_ == PeerBarrier::kChannel) {
       std::lock_guard<std::mutex> lock(channel_->m);
       hipStream_t cs = channel_->stream->get();
       gpu_check(hipEventRecord(channel_->in, stream), "hipEventRecord");
       gpu_check(hipStreamWaitEvent(cs, channel_->in, 0), "hipStreamWaitEvent");
-      dev::launch_peer_barrier(table_->data<unsigned long long*>(),
-                               static_cast<unsigned long long*>(flags_->data()), me_, P_, ++epoch_,
-                               failDev_, timeoutTicks_, cs);
+      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, cs);
       gpu_check(hipEventRecord(channel_->out, cs), "hipEventRecord");
       gpu_check(hipStreamWaitEvent(stream, channel_->out, 0), "hipStreamWaitEvent");
+    } else if (mode_ == PeerBarrier::kStream) {
+      // rounds of this plane in issue order across streams
+      if (lastStream_ != stream && epoch_ > 0)
+        gpu_check(hipStreamWaitEvent(stream, orderEv_, 0), "hipStreamWaitEvent");
+      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, stream);
+      gpu_check(hipEventRecord(orderEv_, stream), "hipEventRecord");
+      lastStream_ = stream;
     } else {
       gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
       comm_->barrier();
@@ -757,7 +780,10 @@ private:
   std::vector<std::array<void*, 3>> peers_;
   std::vector<void*> opened_;
   std::unique_ptr<DeviceBuffer> table_;
+  PeerBarrier mode_ = PeerBarrier::kHost;  // (in-process groups: always host)
   std::shared_ptr<PeerChannel> channel_;
+  hipEvent_t orderEv_ = nullptr;  // "stream" mode: the last round, for the next stream
+  hipStream_t lastStream_ = nullptr;
   unsigned long long epoch_ = 0;
   long long timeoutTicks_ = 0;
   bool readPending_[2] = {false, false};

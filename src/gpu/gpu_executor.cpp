@@ -641,8 +641,8 @@ void GpuExecutor<T>::harvest_stage_times(bool wait) {
 // Failure detection for distributed transforms: the
 // host polls the stream and, every millisecond, the data plane's asynchronous
 // error state (RCCL: ncclCommGetAsyncError; peer writes: barrier timeouts). A
-// failure, or a wait longer than SPFFT_COMM_TIMEOUT seconds (default 120,
-// 0 = no limit), aborts the data plane (ncclCommAbort / barrier kernels released)
+// failure, or a wait longer than SPFFT_COMM_TIMEOUT seconds (default 0 = no
+// limit), aborts the data plane (ncclCommAbort / barrier kernels released)
 // and throws MPIError with the cause in the error detail, instead of leaving
 // the caller blocked forever on a dead peer.
 template <typename T>

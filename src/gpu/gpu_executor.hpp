@@ -203,6 +203,15 @@ private:
   int exchChunks_ = 1;   // K
   int stickBlocks_ = 1;  // I
   bool pipelined() const { return exchChunks_ > 1 || stickBlocks_ > 1; }
+
+public:
+  // The exchange plan (plane chunks K x stick blocks I; peer writes), for
+  // bench.py's modelled times and SPFFT_LOG.
+  int exchange_chunks() const { return exchChunks_; }
+  int exchange_stick_blocks() const { return stickBlocks_; }
+  bool exchange_peer_writes() const { return peerWrites_; }
+
+private:
   double chunkModel_ = 0;  // per-peer bytes of one exchange (chunk model input)
   std::vector<int> planeBounds_;  // K+1 local plane bounds of the chunks
   std::vector<int> stickBounds_;  // I+1 local stick bounds of the z launches

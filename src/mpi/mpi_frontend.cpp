@@ -13,6 +13,7 @@
 #include <climits>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <vector>
 
@@ -44,9 +45,12 @@ bool mpi_finalized() {
 // process-unique id cached on the communicator as an MPI attribute, so every
 // grid built from the same communicator gets the same id, and a communicator
 // created after another was freed (even under a recycled handle) a new one.
+// Guarded: grids may be built concurrently by threads (MPI_THREAD_MULTIPLE).
 unsigned long long domain_of(MPI_Comm comm) {
+  static std::mutex m;
   static int keyval = MPI_KEYVAL_INVALID;
   static unsigned long long next = 0;
+  std::lock_guard<std::mutex> lock(m);
   if (keyval == MPI_KEYVAL_INVALID)
     mpi_check(MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, MPI_COMM_NULL_DELETE_FN, &keyval, nullptr));
   void* v = nullptr;
@@ -172,6 +176,9 @@ public:
           if (t != MPI_DATATYPE_NULL && t != MPI_BYTE) MPI_Type_free(&t);
     }
   };
+  // The layout's byte offset is part of the datatype (an MPI_Aint struct
+  // displacement), so alltoallw's int displacements stay 0 and offsets beyond
+  // 2 GiB work (a slab side of more than 2 GiB per rank).
   static MPI_Datatype strided_type(const StridedLayout& l) {
     std::size_t unit = 1;
     for (std::size_t u : {std::size_t(16), std::size_t(8), std::size_t(4)})
@@ -181,11 +188,15 @@ public:
       }
     if (l.count > static_cast<std::size_t>(INT_MAX) || l.blockBytes / unit > static_cast<std::size_t>(INT_MAX))
       throw OverflowError();
-    MPI_Datatype base = MPI_DATATYPE_NULL, t = MPI_DATATYPE_NULL;
+    MPI_Datatype base = MPI_DATATYPE_NULL, vec = MPI_DATATYPE_NULL, t = MPI_DATATYPE_NULL;
     mpi_check(MPI_Type_contiguous(static_cast<int>(unit), MPI_BYTE, &base));
     mpi_check(MPI_Type_create_hvector(static_cast<int>(l.count), static_cast<int>(l.blockBytes / unit),
-                                      static_cast<MPI_Aint>(l.strideBytes), base, &t));
+                                      static_cast<MPI_Aint>(l.strideBytes), base, &vec));
+    int one = 1;
+    MPI_Aint displ = static_cast<MPI_Aint>(l.offset);
+    mpi_check(MPI_Type_create_struct(1, &one, &displ, &vec, &t));
     mpi_check(MPI_Type_free(&base));
+    mpi_check(MPI_Type_free(&vec));
     mpi_check(MPI_Type_commit(&t));
     return t;
   }
@@ -197,17 +208,13 @@ public:
     w.rc.assign(size_, 0);
     w.rd.assign(size_, 0);
     for (int r = 0; r < size_; ++r) {
-      if (sl[r].offset > static_cast<std::size_t>(INT_MAX) || rl[r].offset > static_cast<std::size_t>(INT_MAX))
-        throw OverflowError();
       if (sl[r].count > 0 && sl[r].blockBytes > 0) {
         w.st[r] = strided_type(sl[r]);
         w.sc[r] = 1;
-        w.sd[r] = static_cast<int>(sl[r].offset);
       }
       if (rl[r].count > 0 && rl[r].blockBytes > 0) {
         w.rt[r] = strided_type(rl[r]);
         w.rc[r] = 1;
-        w.rd[r] = static_cast<int>(rl[r].offset);
       }
     }
   }

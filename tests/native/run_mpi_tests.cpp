@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <stdexcept>
+#include <memory>
 #include <numeric>
 
 #include "spfft/spfft.h"
@@ -24,7 +25,13 @@ struct Setup {
   std::vector<int> stickOwner; // per global value: owning rank
 };
 
-void run_case(SpfftExchangeType ex, SpfftTransformType type, const std::vector<double>& stickW,
+// A grid and its transform, kept alive past run_case by the churn test.
+struct Held {
+  std::unique_ptr<spfft::Grid> grid;
+  std::unique_ptr<spfft::Transform> t;
+};
+
+Held run_case(SpfftExchangeType ex, SpfftTransformType type, const std::vector<double>& stickW,
               const std::vector<double>& planeW, int nx, int ny, int nz, bool centered,
               SpfftProcessingUnitType pu) {
   std::mt19937 rng(123);
@@ -90,9 +97,11 @@ void run_case(SpfftExchangeType ex, SpfftTransformType type, const std::vector<d
   for (int i = 0; i < static_cast<int>(myVals.size()); ++i)
     if (i == 0 || myIdx[3 * i] != myIdx[3 * i - 3] || myIdx[3 * i + 1] != myIdx[3 * i - 2]) ++mySticks;
 
-  spfft::Grid grid(nx, ny, nz, std::max(1, mySticks), myPlanes, pu, 1, MPI_COMM_WORLD, ex);
-  auto t = grid.create_transform(pu, type, nx, ny, nz, myPlanes, static_cast<int>(myVals.size()),
-                                 SPFFT_INDEX_TRIPLETS, myIdx.data());
+  Held held;
+  held.grid.reset(new spfft::Grid(nx, ny, nz, std::max(1, mySticks), myPlanes, pu, 1, MPI_COMM_WORLD, ex));
+  held.t.reset(new spfft::Transform(held.grid->create_transform(
+      pu, type, nx, ny, nz, myPlanes, static_cast<int>(myVals.size()), SPFFT_INDEX_TRIPLETS, myIdx.data())));
+  spfft::Transform& t = *held.t;
   EXPECT_EQ(t.local_z_length(), myPlanes);
   EXPECT_EQ(t.num_global_elements(), static_cast<long long>(n));
   const double tol = (ex == SPFFT_EXCH_BUFFERED_FLOAT || ex == SPFFT_EXCH_COMPACT_BUFFERED_FLOAT) ? 2e-6 : 1e-11;
@@ -117,6 +126,7 @@ void run_case(SpfftExchangeType ex, SpfftTransformType type, const std::vector<d
   int cs = 0;
   MPI_Comm_size(c, &cs);
   EXPECT_EQ(cs, g_size);
+  return held;
 }
 
 const SpfftExchangeType kExchanges[] = {SPFFT_EXCH_DEFAULT,         SPFFT_EXCH_BUFFERED,
@@ -164,6 +174,68 @@ SPFFT_TEST(mpi_gpu_c2c) {
     run_case(ex, SPFFT_TRANS_C2C, only(0), only(g_size - 1), 12, 13, 11, false, SPFFT_PU_GPU);
   }
   run_case(SPFFT_EXCH_DEFAULT, SPFFT_TRANS_R2C, uniform(), uniform(), 12, 11, 13, false, SPFFT_PU_GPU);
+}
+SPFFT_TEST(mpi_gpu_churn) {
+  // every exchange type and both transform types with grids re-created per
+  // case and destroyed by the ranks at different times: rank (case % P) drops
+  // its grid at once, the others keep theirs until two more grids exist.
+  // Destroying a grid needs no peer (reference: src/memory/gpu_array.hpp:88).
+  int nd = spfft_amd_device_count();
+  int ok = nd >= 1 ? 1 : 0, all = 0;
+  MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+  if (!all) {
+    if (g_rank == 0) std::printf("SKIP mpi_gpu_churn: no GPU on some rank\n");
+    return;
+  }
+  if (hipSetDevice(g_rank % nd) != hipSuccess) throw std::runtime_error("hipSetDevice");
+  std::vector<Held> kept;
+  int c = 0;
+  for (auto ex : kExchanges)
+    for (auto type : {SPFFT_TRANS_C2C, SPFFT_TRANS_R2C}) {
+      const std::vector<double> sticks = c % 3 == 0 ? only(c % g_size) : uniform();
+      const std::vector<double> planes = c % 2 == 0 ? uniform() : only(g_size - 1);
+      Held h = run_case(ex, type, sticks, planes, 12 + c % 5, 10 + c % 3, 14 + c % 4, c % 2 == 1,
+                        SPFFT_PU_GPU);
+      if (g_rank == c % g_size) {
+        kept.clear();
+      } else {
+        kept.push_back(std::move(h));
+        if (kept.size() > 2) kept.erase(kept.begin());
+      }
+      ++c;
+    }
+}
+SPFFT_TEST(mpi_alltoallw_offset_beyond_int_max) {
+  // UNBUFFERED host exchange with a layout offset past 2 GiB (a slab side of
+  // more than 2 GiB per rank): the offset travels in the datatype (MPI_Aint),
+  // not in alltoallw's int displacements. The buffers are reserved, not
+  // touched, except for the blocks moved.
+  spfft::Grid grid(4, 4, 4, 16, 4, SPFFT_PU_HOST, 1, MPI_COMM_WORLD, SPFFT_EXCH_UNBUFFERED);
+  auto comm = grid.spfft_communicator();
+  const std::size_t base = (std::size_t(1) << 31) + 4096;  // > INT_MAX
+  const std::size_t block = 64, count = 3, stride = 256;
+  const std::size_t span = base + static_cast<std::size_t>(g_size) * count * stride + stride;
+  std::unique_ptr<unsigned char[]> send(new unsigned char[span]), recv(new unsigned char[span]);
+  std::vector<spfft::StridedLayout> sl(g_size), rl(g_size);
+  for (int r = 0; r < g_size; ++r) {
+    const std::size_t off = base + static_cast<std::size_t>(r) * count * stride;
+    sl[r] = {off, count, block, stride};
+    rl[r] = {off, count, block, stride};
+    for (std::size_t c = 0; c < count; ++c)
+      for (std::size_t b = 0; b < block; ++b) {
+        send[off + c * stride + b] = static_cast<unsigned char>((g_rank * 31 + r * 7 + c * 3 + b) & 0xFF);
+        recv[off + c * stride + b] = 0;
+      }
+  }
+  comm->alltoallw(send.get(), sl.data(), recv.get(), rl.data());
+  bool ok = true;
+  for (int r = 0; r < g_size; ++r) {
+    const std::size_t off = base + static_cast<std::size_t>(r) * count * stride;
+    for (std::size_t c = 0; c < count; ++c)
+      for (std::size_t b = 0; b < block; ++b)
+        ok = ok && recv[off + c * stride + b] == static_cast<unsigned char>((r * 31 + g_rank * 7 + c * 3 + b) & 0xFF);
+  }
+  EXPECT_TRUE(ok);
 }
 SPFFT_TEST(mpi_parameter_mismatch) {
   // ranks disagree on the exchange type -> every rank gets MPIParameterMismatchError

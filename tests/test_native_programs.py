@@ -62,10 +62,14 @@ def test_native_unit_tests_gpu(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nranks", [1, 2, 3])
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4])
 def test_mpi_tests_gpu(gpu, nranks):
-    """MPI front end with GPU grids (mpi_gpu_c2c runs every exchange type): ranks
-    share the box's GPU through the IPC peer-write plane; nothing may be skipped."""
+    """MPI front end with GPU grids (mpi_gpu_c2c runs every exchange type, mpi_gpu_churn
+    every exchange and transform type with grids re-created per case and dropped by the
+    ranks at different times): ranks share the box's GPU through the IPC peer-write
+    plane, the production layout of plane-wave codes that run several ranks per GPU
+    (reference: src/transpose/transpose_mpi_compact_buffered_gpu.cpp:195-219); nothing
+    may be skipped."""
     prog = _prog("spfft_mpi_tests")
     if not os.path.exists(MPIEXEC):
         pytest.skip("mpiexec not available")

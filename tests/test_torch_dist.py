@@ -176,6 +176,11 @@ def test_bench_driver_launch_2ranks_rccl(gpu, monkeypatch):
         assert cfg["stage_ms"][d]["z"] > 0
         assert cfg["exchange_stats"]["ms"][d] > 0 and cfg["exchange_stats"]["GBps_per_rank"][d] > 0
     assert "64^3" in rec["metric"]
+    # the record predicts itself: modelled link / compute / pipelined times per direction
+    m = cfg["model_ms"]
+    assert m["chunks"] >= 1 and m["stick_blocks"] >= 1 and m["bytes_per_peer"] > 0
+    for d in ("backward", "forward"):
+        assert m[d]["link_ms"] > 0 and m[d]["compute_ms"] > 0 and m[d]["predicted_ms"] > 0
 
 
 @pytest.mark.gpu
@@ -253,3 +258,30 @@ def test_ipc_stale_mapping_detected(gpu, monkeypatch):
                              env_extra={"SPFFT_FAULT_IPC_NONCE": "1"}, timeout=180)
     assert code != 0, out[-4000:]
     assert out.count("stale IPC mapping") >= 2, out[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("queues,barrier", [(1, "stream"), (2, "stream"), (1, "channel"), (2, "host")])
+def test_bench_ipc_unbuffered_few_hw_queues(gpu, monkeypatch, queues, barrier):
+    """UNBUFFERED over the IPC peer-write plane, 3 processes, T = 4 transforms per rank
+    on per-transform streams with only 1 or 2 hardware queues per process: every
+    barrier round of a plane keeps its issue order across the streams (stream mode:
+    an event from the previous round's stream; channel mode: one ordered stream per
+    process), so no barrier waits for work queued behind it. SPFFT_PEER_BARRIER=host
+    runs the rounds on the host instead (stream synchronise + communicator barrier)."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", str(queues))
+    monkeypatch.setenv("SPFFT_PEER_BARRIER", barrier)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "3", "--steps", "4", "--warmup", "1",
+           "--size", "64", "--transforms", "4", "--streams", "per-transform", "--exchange", "unbuffered"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    rec = _bench_json(r.stdout)
+    cfg = rec["config"]
+    assert cfg["data_plane"] == "ipc" and cfg["check_error"]["ok"], cfg
+    # the transforms run on the 4 torch streams; the library owns only the peer
+    # channel stream in channel mode
+    assert cfg["library_streams"] == (1 if barrier == "channel" else 0), cfg
