@@ -161,6 +161,35 @@ struct Dft<16, S, T> {
   }
 };
 
+// 32 = 2 x 16: DFT-16 of the even and the odd elements, then one radix-2 layer
+// with the twiddles w32^k (the fp32 line-fast N = 512 shape runs 32 x 16, one
+// LDS exchange per line instead of two).
+template <int S, typename T>
+struct Dft<32, S, T> {
+  static SPFFT_HD void run(cx<T>* v) {
+    cx<T> e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    Dft<16, S, T>::run(e);
+    Dft<16, S, T>::run(o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      cx<T> w;
+      if (k == 0)
+        w = o[k];
+      else if (k == 8)
+        w = rot<S>(o[k]);
+      else
+        w = twc<S>(o[k], T(fftc::C32[k]), T(fftc::S32[k]));
+      v[k] = e[k] + w;
+      v[k + 16] = e[k] - w;
+    }
+  }
+};
+
 // Odd lengths via symmetric pairs: X_k = A_k + S i B_k, X_{R-k} = A_k - S i B_k.
 template <int R, int S, typename T, const double (*CT)[(R - 1) / 2], const double (*ST)[(R - 1) / 2]>
 struct DftOdd {

@@ -149,8 +149,9 @@ struct CtShapeT<float, 1024> {
 // shape (E = 8, 256 threads per 8 lines) doubles the waves per SIMD that the
 // LDS budget allows, which the memory-bound stages turn into bandwidth:
 // measured on MI355X at 256^3 (profiles/r2_s1/shape_ab.txt) x backward 97.6 ->
-// 93.1 us, z backward 79.2 -> 75.3 us, x/y forward -1 us; the forward z stage
-// is slower with it (65.7 -> 71.7 us) and keeps E = 16.
+// 93.1 us, x/y forward -1 us. The row-mapped z stages keep E = 16 (one LDS
+// exchange instead of two): forward 65.7 vs 71.7 us with E = 8 (round 2),
+// backward 67.3 vs 68.0 us, 256^3 R2C 31.7 vs 34.2 us (profiles/r5/ab/c2r_twiddles).
 struct CtShape256E8 {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4, kBudget = kLdsBudget;
 };
@@ -197,11 +198,22 @@ template <>
 struct CtShapeSel<float, 1024, -1, true> : CtShapeF1024W {};
 struct CtShapeF512W {
   static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = 80 * 1024, kMaxThr = 512;
+  static constexpr bool kTwTable = true;
+};
+// fp32 N = 512 line-fast forward engines: 32 elements per lane, radices 32 x 16
+// (one LDS exchange per line instead of two; 256 threads, 16 lines). Measured on
+// MI355X, same box (profiles/r5/ab/f512e32): y forward 218.4 -> 202.5 us (512^3
+// R2C fp32), x forward 575.7 -> 410.0 and y forward 411.2 -> 386.0 us (512^3 C2C
+// fp32). The backward kernels keep the 512-thread radix-16 shape: at 174 VGPRs
+// and half the waves per SIMD the 32-element shape gained nothing there
+// (y backward 219.2 -> 219.7, x backward 377.6 -> 384.1 us).
+struct CtShapeF512E32 {
+  static constexpr int E = 32, R0 = 32, R1 = 16, R2 = 1, kBudget = 80 * 1024, kMaxThr = 256;
 };
 template <>
-struct CtShapeSel<float, 512, 1, true> : CtShapeF512W {};
+struct CtShapeSel<float, 512, -1, true> : CtShapeF512E32 {};
 template <>
-struct CtShapeSel<float, 512, -1, true> : CtShapeF512W {};
+struct CtShapeSel<float, 512, 1, true> : CtShapeF512W {};
 struct CtShapeD512W {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 8, kBudget = 80 * 1024, kMaxThr = 512;
 };
@@ -210,11 +222,21 @@ struct CtShapeSel<double, 512, 1, true> : CtShapeD512W {};
 template <>
 struct CtShapeSel<double, 512, -1, true> : CtShapeD512W {};
 template <>
-struct CtShapeSel<double, 256, 1, false> : CtShape256E8 {};
-template <>
 struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
+
+// Twiddles of a pass: one table entry per butterfly group and its powers
+// formed in registers (twiddle_powers), unless the shape declares
+// kTwTable = true (every power read from the table). Powers measured on MI355X
+// (profiles/r5/ab/twpow): 256^3 C2C fp32 kernel sum 282.7 -> 262.6 us, fp64
+// 494.6 -> 486.0 us, 512^3 R2C fp32 z forward 150.5 -> 111.1 us. The wide fp32
+// N = 512 backward shape keeps the table: powers took its y stage from 125 to
+// 130 VGPRs, past the occupancy step of its 512-thread workgroups (221 -> 295 us).
+template <class Sh, class = void>
+struct ShapeTwTable : std::false_type {};
+template <class Sh>
+struct ShapeTwTable<Sh, std::void_t<decltype(Sh::kTwTable)>> : std::integral_constant<bool, Sh::kTwTable> {};
 
 // Workgroup size cap of a shape: Sh::kMaxThr where a shape declares it (wide
 // 512-thread shapes), else kMaxThreads.
@@ -273,6 +295,21 @@ __host__ __device__ constexpr int lf_padded_stride(int n, int b, int shift) {
   return ls;
 }
 
+// Twiddles w^1 .. w^(R-1) of one radix-R butterfly group from w = w^1 (one
+// table load instead of R - 1): products of at most log2(R) + 1 factors, so
+// the error stays within a few ulp.
+template <int R, typename T>
+__device__ __forceinline__ void twiddle_powers(cx<T> w, cx<T> (&p)[R - 1]) {
+  p[0] = w;
+#pragma unroll
+  for (int r = 2; r < R; ++r) {
+    // r = a + b with a the largest power of two below r (or r / 2 for powers of two)
+    int a = 1;
+    while (a * 2 < r) a *= 2;
+    p[r - 1] = cmul(p[a - 1], p[r - a - 1]);
+  }
+}
+
 // LF (line-fast) selects the lane -> (line b, lane t) mapping:
 //  false: t fastest (a line's TP lanes adjacent; row-contiguous global access),
 //  true:  b fastest (B lines adjacent; column-contiguous global access, e.g. a
@@ -294,6 +331,7 @@ struct FftCT {
   static constexpr int LS = LF ? lf_padded_stride<T>(N, B, PS) : LS0;
   static constexpr int NT = B * TP;
   static constexpr int RL = Sh::R2 > 1 ? Sh::R2 : (Sh::R1 > 1 ? Sh::R1 : Sh::R0);
+  static constexpr bool kTwPow = !ShapeTwTable<Sh>::value;
 
   static constexpr int lines() { return B; }
   static constexpr int threads() { return NT; }
@@ -312,9 +350,16 @@ struct FftCT {
       if (NS > 1) {
         const int j = t + k * TP;
         const int kk = j % NS;
+        if constexpr (kTwPow) {
+          cx<T> p[R - 1];
+          twiddle_powers<R>(tw[kk * (N / (NS * R))], p);
 #pragma unroll
-        for (int r = 1; r < R; ++r)
-          v[k * R + r] = twm<S>(v[k * R + r], tw[kk * r * (N / (NS * R))]);
+          for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], p[r - 1]);
+        } else {
+#pragma unroll
+          for (int r = 1; r < R; ++r)
+            v[k * R + r] = twm<S>(v[k * R + r], tw[kk * r * (N / (NS * R))]);
+        }
       }
       Dft<R, S, T>::run(&v[k * R]);
     }
@@ -346,25 +391,37 @@ struct FftCT {
   // read (an L1/L2 hit) overlaps the exchange instead of following it.
   // (not for the 32-element shapes of N = 1024: their registers are full)
   static constexpr bool kTwPrefetch = TwPre && E <= 16;
+  // (kTwPow: one table entry per butterfly group, its powers formed in compute_tw)
   template <int R, int NS>
   struct PassTw {
-    cx<TwT> w[(E / R) * (R - 1)];
+    cx<TwT> w[kTwPow ? E / R : (E / R) * (R - 1)];
   };
   template <int R, int NS>
   __device__ static void fetch_tw(PassTw<R, NS>& p, int t, const cx<TwT>* __restrict__ tw) {
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {
       const int kk = (t + k * TP) % NS;
+      if constexpr (kTwPow) {
+        p.w[k] = tw[kk * (N / (NS * R))];
+      } else {
 #pragma unroll
-      for (int r = 1; r < R; ++r) p.w[k * (R - 1) + r - 1] = tw[kk * r * (N / (NS * R))];
+        for (int r = 1; r < R; ++r) p.w[k * (R - 1) + r - 1] = tw[kk * r * (N / (NS * R))];
+      }
     }
   }
   template <int R, int NS>
   __device__ static void compute_tw(cx<T> (&v)[E], const PassTw<R, NS>& p) {
 #pragma unroll
     for (int k = 0; k < E / R; ++k) {
+      if constexpr (kTwPow) {
+        cx<T> w[R - 1];
+        twiddle_powers<R>(p.w[k], w);
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], p.w[k * (R - 1) + r - 1]);
+        for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], w[r - 1]);
+      } else {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[k * R + r] = twm<S>(v[k * R + r], p.w[k * (R - 1) + r - 1]);
+      }
       Dft<R, S, T>::run(&v[k * R]);
     }
   }

@@ -1271,6 +1271,16 @@ __global__ void __launch_bounds__(Eng::kBlock)
 //   R2C: Y = DFT_h(y),  X[k] = (Y[k] + conj Y[h-k])/2 + w^k (Y[k] - conj Y[h-k])/(2i)
 // with w = exp(S 2 pi i / n); the imaginary parts of X[0] and X[h] are ignored
 // (they cannot contribute to a real signal), as in the complex C2R path.
+// first-pass radix of a compile-time engine (0: mixed-radix engines)
+template <class F, class = void>
+struct FirstRadix {
+  static constexpr int value = 0;
+};
+template <class F>
+struct FirstRadix<F, std::void_t<typename F::Sh>> {
+  static constexpr int value = F::Sh::R0;
+};
+
 template <class Eng, typename T>
 __global__ void __launch_bounds__(Eng::kBlock)
     x_backward_c2r_kernel(Eng eng, XArgs a, const cx<T>* __restrict__ inter, T* __restrict__ space,
@@ -1301,7 +1311,13 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const int c = dense ? (k < nFreq ? k : -1) : xCol[k];
       return (c < 0 || b >= yl) ? czero<T>() : src[c * rowStride + b];
     };
-    eng.global_to_lds(lds, twh, [&](int b, int k) -> cx<T> {
+    // twiddle w^k of position k = t + off, off = kk*TP + r*(h/R0): the table
+    // entry of t + kk*TP times the compile-time root exp(-i pi r / R0), so a
+    // lane loads one entry per kk instead of one per element: 131 -> 115 VGPRs
+    // (fp32 h = 256), x backward at 512^3 R2C fp32 259.2 -> 217.9 us, 256^3 R2C
+    // fp64 55.5 -> 54.5 us (profiles/r5/ab/c2r_twiddles)
+    constexpr int R0 = FirstRadix<typename Eng::F>::value, Q = R0 ? Eng::kN / R0 : 1;
+    eng.global_to_lds(lds, twh, [&](int b, int k, int off) -> cx<T> {
       cx<T> xk = col(k, b);
       cx<T> xm = col(h - k, b);
       if (k == 0) {
@@ -1309,7 +1325,16 @@ __global__ void __launch_bounds__(Eng::kBlock)
         xm.y = T(0);
       }
       const cx<T> xmc = conj(xm);
-      return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, twn[k]));
+      const int r = off / Q;
+      cx<T> w = twn[k - r * Q];
+      if constexpr (R0 == 16) {
+        if (r) w = cmul(w, mk<T>(T(fftc::C32[r & 15]), T(-fftc::S32[r & 15])));
+      } else if constexpr (R0 == 8) {
+        if (r) w = cmul(w, mk<T>(T(fftc::C16[r & 15]), T(-fftc::S16[r & 15])));
+      } else {
+        w = twn[k];
+      }
+      return (xk + xmc) + rot<+1>(twm<+1>(xk - xmc, w));
     });
     cx<T>* out = reinterpret_cast<cx<T>*>(space + (static_cast<long long>(zl) * a.Y + y0) * n);
     copy_out<Eng>(lds, yl * h, [&](int idx) {
