@@ -336,8 +336,8 @@ def main():
     n_devices = min(world, ndev)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * T * a.steps / elapsed
-    # the reference's FFT calls alone (rocFFT via torch.fft)
-    # on one MI355X, an upper bound on its throughput for the headline config;
+    # the reference's FFT calls alone (rocFFT via
+    # torch.fft) on one MI355X, an upper bound on its throughput for the headline config;
     # no measured reference exists for other configs or for N > 1 GPUs
     headline = (n == 256 and a.cutoff == 0.5 and a.type == "c2c" and not single)
     # comparator per protocol: the reference algorithm's rocFFT calls alone on one
@@ -360,7 +360,7 @@ def main():
             "vs_baseline": vs_baseline,
             "vs_baseline_basis": (f"value / {ref_rate:.1f}: the reference algorithm's rocFFT calls "
                                   f"alone on one MI355X with the same {T} transform(s) per step "
-                                  f"(BASELINE.md B7, tools/ref_pipeline_bench.py --transforms {T})"
+                                  f"(BASELINE.md {'B7' if T == 1 else 'B7-T4'}, tools/ref_pipeline_bench.py --transforms {T})"
                                   if vs_baseline else None),
             "dtype": "fp32" if single else "fp64",
             "data": "synthetic (random complex values on the spherical-cutoff index set)",

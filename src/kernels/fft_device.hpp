@@ -221,6 +221,9 @@ template <>
 struct CtShapeSel<double, 512, 1, true> : CtShapeD512W {};
 template <>
 struct CtShapeSel<double, 512, -1, true> : CtShapeD512W {};
+// (re-measured in round 5 with twiddle powers: the 16-element line-fast shape,
+// 128 threads per 8 lines, is still slower, x backward 92.0 -> 99.0 us,
+// profiles/r5/ab/lf16)
 template <>
 struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
 template <>
