@@ -41,7 +41,7 @@ REF_FFT_ONLY_256_BY_T = {1: 2210.2, 4: 2418.3}  # profiles/r3/comparator/
 LINK_GBPS = 70.0
 
 
-def _model(stages, sent_per_rank, world, chunks, blocks):
+def _model(stages, sent_per_rank, world, chunks, blocks, relays=0):
     """Modelled per-direction times of a distributed step (README, "Multi-GPU
     scaling"): every rank sends sent/(N-1) bytes to each peer over its own link, all
     links at once, so the exchange takes link_ms = sent/(N-1) / LINK_GBPS; the
@@ -50,9 +50,12 @@ def _model(stages, sent_per_rank, world, chunks, blocks):
     predicted = max(link, compute) + compute / (K * I) (unpipelined: link + compute).
     The driver's measured ms_per_step / (2 T) can be read against `predicted_ms`."""
     per_peer = sent_per_rank / max(1, world - 1)
-    link_ms = per_peer / (LINK_GBPS * 1e9) * 1e3
+    # relay plane: every link direction carries (N - 1) / (N - 1 + K) of a
+    # peer message, in two host-synchronous hops (push, pull)
+    share = (world - 1) / (world - 1 + relays) if relays else 1.0
+    link_ms = per_peer * share / (LINK_GBPS * 1e9) * 1e3 * (2 if relays else 1)
     out = {"link_GBps_assumed": LINK_GBPS, "bytes_per_peer": per_peer,
-           "chunks": chunks, "stick_blocks": blocks}
+           "chunks": chunks, "stick_blocks": blocks, "relay_gpus": relays}
     for d in ("backward", "forward"):
         st = stages.get(d, {})
         compute = sum(v for k, v in st.items() if k not in ("exchange", "exchange-span", "exchange-tail", "total"))
@@ -327,8 +330,8 @@ def main():
         exch["max_bytes_sent_per_rank"] = float(e.item())
     model = None
     if world > 1 and stages:
-        chunks, blocks, peer_writes = t.exchange_plan()
-        model = _model(stages, exch["max_bytes_sent_per_rank"], world, chunks, blocks)
+        chunks, blocks, peer_writes, relays = t.exchange_plan()
+        model = _model(stages, exch["max_bytes_sent_per_rank"], world, chunks, blocks, relays)
         model["peer_writes"] = peer_writes
         model["shared_device"] = min(world, ndev) < world
     # ranks that share a device (rehearsal on a small box) are not a multi-GPU

@@ -76,14 +76,16 @@ SPFFT_EXPORT SpfftError spfft_amd_rccl_communicators(int* count);
  * channel streams (one per shared communicator). */
 SPFFT_EXPORT SpfftError spfft_amd_library_streams(int* count);
 /* Exchange plan of a GPU transform: plane chunks K and stick blocks I of the
- * pipelined all-to-all (1 and 1: one exchange per direction), and whether the
- * stage kernels write into the peers directly (UNBUFFERED / IPC plane). Host
- * transforms report 0, 0, 0. */
+ * pipelined all-to-all (1 and 1: one exchange per direction), whether the
+ * stage kernels write into the peers directly (UNBUFFERED / IPC plane), and
+ * the number of idle GPUs the exchange relays through (relay plane). Host
+ * transforms report zeros. */
 SPFFT_EXPORT SpfftError spfft_amd_transform_exchange_plan(SpfftTransform transform, int* chunks,
-                                                          int* stickBlocks, int* peerWrites);
+                                                          int* stickBlocks, int* peerWrites,
+                                                          int* relays);
 SPFFT_EXPORT SpfftError spfft_amd_float_transform_exchange_plan(SpfftFloatTransform transform,
                                                                 int* chunks, int* stickBlocks,
-                                                                int* peerWrites);
+                                                                int* peerWrites, int* relays);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_exchange_type(SpfftFloatGrid grid,
                                                            SpfftExchangeType* type);
 

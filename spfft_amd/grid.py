@@ -356,11 +356,11 @@ class _TransformBase:
         _check(self._prec.amd_fn("transform_synchronize")(self._h))
 
     def exchange_plan(self):
-        """(plane chunks K, stick blocks I, peer writes) of the GPU exchange pipeline."""
-        k, i, pw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        """(plane chunks K, stick blocks I, peer writes, relay GPUs) of the GPU exchange."""
+        k, i, pw, rl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(self._prec.amd_fn("transform_exchange_plan")(self._h, ctypes.byref(k), ctypes.byref(i),
-                                                            ctypes.byref(pw)))
-        return k.value, i.value, bool(pw.value)
+                                                            ctypes.byref(pw), ctypes.byref(rl)))
+        return k.value, i.value, bool(pw.value), rl.value
 
     def rank_z_range(self, rank: int):
         off, ln = ctypes.c_int(), ctypes.c_int()

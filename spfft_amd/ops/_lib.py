@@ -97,8 +97,8 @@ def _prototypes(lib):
     sig["spfft_amd_float_transform_reset_stream"] = [V]
     sig["spfft_amd_float_transform_synchronize"] = [V]
     sig["spfft_amd_transform_local_z_offset_rank"] = [V, I, c_int_p, c_int_p]
-    sig["spfft_amd_transform_exchange_plan"] = [V, c_int_p, c_int_p, c_int_p]
-    sig["spfft_amd_float_transform_exchange_plan"] = [V, c_int_p, c_int_p, c_int_p]
+    sig["spfft_amd_transform_exchange_plan"] = [V, c_int_p, c_int_p, c_int_p, c_int_p]
+    sig["spfft_amd_float_transform_exchange_plan"] = [V, c_int_p, c_int_p, c_int_p, c_int_p]
     sig["spfft_amd_transform_space_domain_dlpack"] = [V, I, c_void_pp]
     sig["spfft_amd_float_transform_space_domain_dlpack"] = [V, I, c_void_pp]
     sig["spfft_amd_transform_forward_xy"] = [V, I]

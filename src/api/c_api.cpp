@@ -147,11 +147,12 @@ const char* data_plane_of(Impl& impl) {
 
 namespace {
 template <typename T, class X>
-void exchange_plan_of(X& x, int* chunks, int* stickBlocks, int* peerWrites) {
+void exchange_plan_of(X& x, int* chunks, int* stickBlocks, int* peerWrites, int* relays) {
   auto* g = x.impl()->gpu();
   *chunks = g ? g->exchange_chunks() : 0;
   *stickBlocks = g ? g->exchange_stick_blocks() : 0;
   *peerWrites = g && g->exchange_peer_writes() ? 1 : 0;
+  *relays = g && x.impl()->plan().size > 1 ? x.impl()->grid()->device_comm().relay_count() : 0;
 }
 }  // namespace
 
@@ -398,16 +399,16 @@ SpfftError spfft_amd_library_streams(int* count) {
 }
 
 SpfftError spfft_amd_transform_exchange_plan(SpfftTransform t, int* chunks, int* stickBlocks,
-                                             int* peerWrites) {
-  if (!chunks || !stickBlocks || !peerWrites) return SPFFT_INVALID_PARAMETER_ERROR;
+                                             int* peerWrites, int* relays) {
+  if (!chunks || !stickBlocks || !peerWrites || !relays) return SPFFT_INVALID_PARAMETER_ERROR;
   return with_handle<Transform>(
-      t, [&](Transform& x) { exchange_plan_of<double>(x, chunks, stickBlocks, peerWrites); });
+      t, [&](Transform& x) { exchange_plan_of<double>(x, chunks, stickBlocks, peerWrites, relays); });
 }
 SpfftError spfft_amd_float_transform_exchange_plan(SpfftFloatTransform t, int* chunks,
-                                                   int* stickBlocks, int* peerWrites) {
-  if (!chunks || !stickBlocks || !peerWrites) return SPFFT_INVALID_PARAMETER_ERROR;
+                                                   int* stickBlocks, int* peerWrites, int* relays) {
+  if (!chunks || !stickBlocks || !peerWrites || !relays) return SPFFT_INVALID_PARAMETER_ERROR;
   return with_handle<TransformFloat>(
-      t, [&](TransformFloat& x) { exchange_plan_of<float>(x, chunks, stickBlocks, peerWrites); });
+      t, [&](TransformFloat& x) { exchange_plan_of<float>(x, chunks, stickBlocks, peerWrites, relays); });
 }
 
 SpfftError spfft_amd_transform_set_stream(SpfftTransform t, void* stream, int synchronous) {

@@ -21,6 +21,7 @@
 #include "gpu/gpu_runtime.hpp"
 #include "gpu/ipc_arena.hpp"
 #include "kernels/peer_sync.hpp"
+#include "kernels/relay_copy.hpp"
 #include "spfft/exceptions.hpp"
 
 namespace spfft {
@@ -789,6 +790,274 @@ private:
   bool readPending_[2] = {false, false};
 };
 
+// ------------------------------------------------------------ relay routing
+// Ranks on distinct GPUs of one node that leave other GPUs of the node idle
+// (the driver's N = 2 and N = 4 runs on an 8-GPU node): every peer message is
+// split into a direct part and one part per idle GPU c, which goes p -> c -> q
+// over two xGMI links that the direct route does not use. With K idle GPUs and
+// N ranks each pair's message is cut into N - 1 + K shares, the direct link
+// carrying N - 1 of them and each relay one, which balances the load of every
+// link direction (p -> q carries N - 1 shares; p -> c and c -> q carry one
+// share per peer, N - 1 in all): the exchange takes (N - 1) / (N - 1 + K) of
+// the direct-only link time, 1/7 at N = 2 on 8 GPUs, 3/7 at N = 4.
+//
+// Two host-synchronous phases per exchange, each one multi-segment copy
+// launch on the caller's device (kernels/relay_copy.hip):
+//  1. push: the relay shares into this rank's relay buffers on the idle GPUs
+//     (memory this process allocates there, from the IPC arena, and exports
+//     to the peers);
+//  2. pull, after a communicator barrier: each receiver copies its direct part
+//     out of the sender's send side and its relay shares out of the senders'
+//     relay buffers; a second barrier frees the buffers.
+// No GPU writes into another rank's GPU memory: a receiver's L2 may hold lines
+// of its own buffers from an earlier read, which a remote store would leave
+// stale. Remote memory is only read (its lines are dropped by the copy
+// kernel's system-scope acquire) or written on an idle GPU that runs no
+// kernels.
+// Every rank computes every rank's split from the allgathered transfer lists,
+// so the layouts agree without further messages. Shares are multiples of 16
+// bytes; messages below SPFFT_RELAY_MIN_BYTES (default 1 MiB) go direct only.
+// SPFFT_RELAY: "auto" (default: on when idle GPUs are visible), "0" off,
+// "force" (relay through K = SPFFT_RELAY_VIRTUAL virtual relays on the rank's
+// own GPU: exercises the layouts and phases on a one-GPU box).
+class RelayDeviceComm : public DeviceComm {
+public:
+  RelayDeviceComm(const std::shared_ptr<Communicator>& comm, int device, const std::size_t bytes[2],
+                  const std::vector<int>& relayDevices)
+      : comm_(comm), device_(device), me_(comm->rank()), P_(comm->size()),
+        K_(static_cast<int>(relayDevices.size())), relayDev_(relayDevices) {
+    DeviceGuard guard(device);
+    const char* e = std::getenv("SPFFT_RELAY_MIN_BYTES");
+    minBytes_ = e && *e ? static_cast<long long>(std::atof(e)) : (1LL << 20);
+    // relay capacity per idle GPU: a rank's relayed bytes per relay are at
+    // most its send side / (N - 1 + K)
+    const std::size_t side = std::max(bytes[0], bytes[1]);
+    relayCap_ = side / static_cast<std::size_t>(std::max(1, P_ - 1 + K_)) + 4096;
+    struct Announce {
+      IpcExport e[2 + kMaxRelays];
+    };
+    struct Outcome {
+      int ok;
+      char why[200];
+    };
+    Announce mine{};
+    Outcome res{1, {0}};
+    if (K_ > kMaxRelays) throw InternalError();
+    try {
+      // the copy kernels read other GPUs' memory: peer access to every device
+      int ndev = 0;
+      if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+      for (int d = 0; d < ndev; ++d)
+        if (d != device) (void)hipDeviceEnablePeerAccess(d, 0);
+      (void)hipGetLastError();
+      for (int i = 0; i < 2; ++i)
+        if (bytes[i] > 0) {
+          sides_[i] = ipc_acquire(device, bytes[i], false);
+          mine.e[i] = sides_[i]->describe();
+        }
+      for (int c = 0; c < K_; ++c) {
+        if (relayDev_[c] != device) {
+          int can = 0;
+          gpu_check(hipDeviceCanAccessPeer(&can, device, relayDev_[c]), "hipDeviceCanAccessPeer");
+          if (!can) throw GPUError();
+        }
+        relay_.push_back(ipc_acquire(relayDev_[c], relayCap_, false));
+        mine.e[2 + c] = relay_.back()->describe();
+      }
+    } catch (const std::exception& ex) {
+      res.ok = 0;
+      std::snprintf(res.why, sizeof(res.why), "relay setup: %s %s", ex.what(), error_detail().c_str());
+    }
+    std::vector<Announce> all(P_);
+    comm_->allgather(&mine, all.data(), sizeof(Announce));
+    peers_.assign(P_, std::vector<char*>(2 + K_, nullptr));
+    if (res.ok) {
+      try {
+        for (int q = 0; q < P_ && res.ok; ++q)
+          for (int i = 0; i < 2 + K_ && res.ok; ++i) {
+            if (q == me_) {
+              peers_[q][i] = static_cast<char*>(i < 2 ? (sides_[i] ? sides_[i]->data() : nullptr)
+                                                      : relay_[i - 2]->data());
+              continue;
+            }
+            if (!all[q].e[i].valid) continue;
+            std::string why;
+            void* p = ipc_open_checked(all[q].e[i], &why);
+            if (!p) {
+              res.ok = 0;
+              std::snprintf(res.why, sizeof(res.why), "rank %d <- rank %d: %s", me_, q, why.c_str());
+              break;
+            }
+            opened_.push_back(p);
+            peers_[q][i] = static_cast<char*>(p);
+          }
+      } catch (const std::exception& ex) {
+        res.ok = 0;
+        std::snprintf(res.why, sizeof(res.why), "hipIpcOpenMemHandle: %s %s", ex.what(), error_detail().c_str());
+      }
+    }
+    std::vector<Outcome> outs(P_);
+    comm_->allgather(&res, outs.data(), sizeof(Outcome));
+    for (const Outcome& o : outs) {
+      if (o.ok) continue;
+      for (void* p : opened_) ipc_close(p);
+      opened_.clear();
+      set_error_detail(std::string("relay data plane: ") + o.why);
+      throw MPIError();
+    }
+    const std::size_t maxSegs = static_cast<std::size_t>(2 * P_ + 2) * (1 + K_) + 8;
+    segsHost_.resize(maxSegs);
+    segsDev_.reset(new DeviceBuffer(maxSegs * sizeof(dev::CopySeg)));
+    gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    comm_->barrier();
+  }
+
+  ~RelayDeviceComm() override {
+    if (process_exiting()) return;
+    try {
+      DeviceGuard guard(device_);
+      for (void* p : opened_) ipc_close(p);
+    } catch (...) {
+    }
+  }
+
+  void exchange(const void* send, void* recv, const std::vector<Transfer>& xs, hipStream_t stream,
+                const ExchangeSync* sync) override {
+    SPFFT_TIMED_SCOPE("relay_exchange");
+    DeviceGuard guard(device_);
+    const int recvSlot = recv == local_buffer(0) ? 0 : (recv == local_buffer(1) ? 1 : -1);
+    const int sendSlot = 1 - recvSlot;
+    // the grid's exchange sides only
+    if (recvSlot < 0 || send != local_buffer(sendSlot)) throw InternalError();
+    sync_begin(sync, stream);
+    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    // every rank's transfer list (fixed size: own block + one send and one
+    // receive per peer)
+    const int W = 2 * P_ + 1;
+    std::vector<Transfer> wire(W, Transfer{-1, 0, 0, 0, 0});
+    if (static_cast<int>(xs.size()) > W) throw InternalError();
+    std::copy(xs.begin(), xs.end(), wire.begin());
+    std::vector<Transfer> all(static_cast<std::size_t>(W) * P_);
+    comm_->allgather(wire.data(), all.data(), sizeof(Transfer) * W);
+    // matched pairs p -> q: send offset, receive offset, bytes (NCCL matching
+    // rule: one send and one receive per ordered pair in these lists)
+    std::vector<long long> so(P_ * P_, -1), ro(P_ * P_, -1), nb(P_ * P_, 0);
+    for (int p = 0; p < P_; ++p)
+      for (int i = 0; i < W; ++i) {
+        const Transfer& t = all[static_cast<std::size_t>(p) * W + i];
+        if (t.kind == Transfer::kSend) {
+          so[p * P_ + t.peer] = t.offset;
+          nb[p * P_ + t.peer] = t.bytes;
+        } else if (t.kind == Transfer::kRecv) {
+          ro[t.peer * P_ + p] = t.offset;
+        }
+      }
+    // shares: base per relay (16-byte multiple), the direct part the rest
+    std::vector<long long> base(P_ * P_, 0), roff(P_ * P_, 0);
+    for (int p = 0; p < P_; ++p) {
+      long long used = 0;
+      for (int q = 0; q < P_; ++q) {
+        const long long m = nb[p * P_ + q];
+        long long b = 0;
+        if (q != p && K_ > 0 && m >= minBytes_) b = (m / (P_ - 1 + K_)) / 16 * 16;
+        if (used + b > static_cast<long long>(relayCap_)) b = 0;
+        base[p * P_ + q] = b;
+        roff[p * P_ + q] = used;
+        used += b;
+      }
+    }
+    const char* s = static_cast<const char*>(send);
+    char* r = static_cast<char*>(recv);
+    for (int p = 0; p < P_; ++p)
+      for (int q = 0; q < P_; ++q)
+        if (p != q && nb[p * P_ + q] > 0 && (so[p * P_ + q] < 0 || ro[p * P_ + q] < 0)) mismatch();
+    // phase 1: own block, relay pushes
+    segCount_ = 0;
+    for (const Transfer& t : xs)
+      if (t.kind == Transfer::kLocal) add_seg(s + t.offset, r + t.dstOffset, t.bytes);
+    for (int q = 0; q < P_; ++q) {
+      const int k = me_ * P_ + q;
+      if (q == me_ || base[k] == 0) continue;
+      const long long direct = nb[k] - K_ * base[k];
+      for (int c = 0; c < K_; ++c)
+        add_seg(s + so[k] + direct + c * base[k], peers_[me_][2 + c] + roff[k], base[k]);
+    }
+    if (segCount_ > 0) {
+      run_segs(stream);
+      gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    }
+    comm_->barrier();
+    // phase 2: pull the direct parts and the relayed shares addressed here
+    segCount_ = 0;
+    for (int p = 0; p < P_; ++p) {
+      const int k = p * P_ + me_;
+      if (p == me_ || nb[k] == 0) continue;
+      const long long direct = nb[k] - K_ * base[k];
+      add_seg(peers_[p][sendSlot] + so[k], r + ro[k], direct);
+      for (int c = 0; c < K_ && base[k] > 0; ++c)
+        add_seg(peers_[p][2 + c] + roff[k], r + ro[k] + direct + c * base[k], base[k]);
+    }
+    if (segCount_ > 0) {
+      run_segs(stream);
+      gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    }
+    comm_->barrier();  // send sides and relay buffers are free again
+    sync_end(sync, stream);
+  }
+  int plane_rank() const override { return me_; }
+  int plane_size() const override { return P_; }
+  bool host_synchronous() const override { return true; }
+  int max_pipeline_steps() const override { return 1; }
+  void* local_buffer(int slot) const override {
+    if (slot < 0 || slot > 1 || !sides_[slot]) return nullptr;
+    return sides_[slot]->data();
+  }
+  const char* kind() const override { return "relay"; }
+  std::string describe() const override {
+    std::string d = "relay (" + std::to_string(P_) + " ranks, " + std::to_string(K_) + " relay GPU(s):";
+    for (int c : relayDev_) d += " " + std::to_string(c);
+    return d + ")";
+  }
+  int relay_count() const override { return K_; }
+
+private:
+  static constexpr int kMaxRelays = 8;
+  [[noreturn]] void mismatch() {
+    set_error_detail("relay exchange: transfer lists of the ranks do not match");
+    throw MPIError();
+  }
+  void add_seg(const char* src, char* dst, long long bytes) {
+    if (bytes <= 0) return;
+    if (segCount_ >= segsHost_.size()) throw InternalError();
+    segsHost_[segCount_++] = dev::CopySeg{src, dst, static_cast<unsigned long long>(bytes), 0};
+  }
+  void run_segs(hipStream_t stream) {
+    long long chunks = 0;
+    for (std::size_t i = 0; i < segCount_; ++i) {
+      segsHost_[i].firstChunk = chunks;
+      chunks += (static_cast<long long>(segsHost_[i].bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
+    }
+    if (segCount_ == 0) return;
+    gpu_check(hipMemcpyAsync(segsDev_->data(), segsHost_.data(), segCount_ * sizeof(dev::CopySeg),
+                             hipMemcpyHostToDevice, stream),
+              "hipMemcpyAsync");
+    dev::launch_multi_copy(segsDev_->data<dev::CopySeg>(), static_cast<int>(segCount_), chunks, stream);
+  }
+
+  std::shared_ptr<Communicator> comm_;
+  int device_, me_, P_, K_;
+  std::vector<int> relayDev_;
+  long long minBytes_ = 0;
+  std::size_t relayCap_ = 0;
+  std::unique_ptr<IpcLease> sides_[2];
+  std::vector<std::unique_ptr<IpcLease>> relay_;
+  std::vector<std::vector<char*>> peers_;  // [rank][0: stick side, 1: slab side, 2 + c: relay c]
+  std::vector<void*> opened_;
+  std::vector<dev::CopySeg> segsHost_;
+  std::size_t segCount_ = 0;
+  std::unique_ptr<DeviceBuffer> segsDev_;
+};
+
 struct NodeInfo {
   std::uint64_t host;
   long long pid;
@@ -796,7 +1065,86 @@ struct NodeInfo {
   unsigned long long channelDomain;  // Communicator::channel_domain
   int prefer;  // SPFFT_GPU_EXCHANGE: 0 auto, 1 rccl, 2 peer (ipc)
   int fault;   // SPFFT_FAULT_RCCL_INIT (rank 0's value is used everywhere)
+  int relay;   // SPFFT_RELAY: 0 auto, 1 off, 2 force (virtual relays)
+  int relayVirtual;  // SPFFT_RELAY_VIRTUAL
+  unsigned long long stickBytes;  // this rank's stick side (per-peer message estimate)
 };
+
+// SPFFT_RELAY=auto: whether relaying through K idle GPUs beats the direct
+// links for per-peer messages of m bytes among n ranks. Direct: m at one link's
+// rate; relay: two hops of (n - 1) / (n - 1 + K) of m each, plus ~100 us of
+// host round trips (two stream synchronisations, two barriers). Relay is
+// chosen when it models at least 20% faster: N = 2 at 256^3 fp64 (52 MB per
+// peer, K = 6: 750 vs 315 us) relays; N = 4 (13 MB, K = 4: 190 vs 260 us)
+// and small problems stay on RCCL.
+bool relay_pays(double m, int n, int k) {
+  constexpr double kLinkBytesPerUs = 70e3, kHostUs = 100.0;
+  const double direct = m / kLinkBytesPerUs;
+  const double relay = 2.0 * m * (n - 1) / (n - 1 + k) / kLinkBytesPerUs + kHostUs;
+  return relay < 0.8 * direct;
+}
+
+int env_relay() {
+  const char* e = std::getenv("SPFFT_RELAY");
+  const std::string v = e ? e : "";
+  return v == "0" || v == "off" ? 1 : (v == "force" ? 2 : 0);
+}
+
+// PCI location of a device ordinal of this process
+struct PciId {
+  int domain, bus, device;
+  bool operator==(const PciId& o) const { return domain == o.domain && bus == o.bus && device == o.device; }
+};
+PciId pci_of(int ordinal) {
+  PciId id{-1, -1, -1};
+  (void)hipDeviceGetAttribute(&id.domain, hipDeviceAttributePciDomainID, ordinal);
+  (void)hipDeviceGetAttribute(&id.bus, hipDeviceAttributePciBusId, ordinal);
+  (void)hipDeviceGetAttribute(&id.device, hipDeviceAttributePciDeviceId, ordinal);
+  (void)hipGetLastError();
+  return id;
+}
+
+// Collective. The GPUs of this node that no rank of the group runs on and
+// that every rank can see, as this process's ordinals, in rank 0's order
+// (at most kMaxRelay).
+std::vector<int> idle_devices(Communicator& comm, const std::vector<PciId>& used) {
+  constexpr int kMaxDev = 16, kMaxRelay = 8;
+  struct Visible {
+    int n;
+    PciId id[kMaxDev];
+  };
+  Visible mine{};
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+  (void)hipGetLastError();
+  mine.n = std::min(count, kMaxDev);
+  for (int d = 0; d < mine.n; ++d) mine.id[d] = pci_of(d);
+  const int P = comm.size();
+  std::vector<Visible> all(P);
+  comm.allgather(&mine, all.data(), sizeof(Visible));
+  // candidates: rank 0's devices no rank uses
+  std::vector<PciId> cand;
+  for (int d = 0; d < all[0].n; ++d) {
+    bool inUse = false;
+    for (const PciId& u : used) inUse = inUse || u == all[0].id[d];
+    if (!inUse && static_cast<int>(cand.size()) < kMaxRelay) cand.push_back(all[0].id[d]);
+  }
+  // keep those every rank sees; this process's ordinal of each
+  std::vector<int> out;
+  for (const PciId& c : cand) {
+    int mineOrd = -1;
+    bool everyone = true;
+    for (int q = 0; q < P; ++q) {
+      int ord = -1;
+      for (int d = 0; d < all[q].n; ++d)
+        if (all[q].id[d] == c) ord = d;
+      everyone = everyone && ord >= 0;
+      if (q == comm.rank()) mineOrd = ord;
+    }
+    if (everyone) out.push_back(mineOrd);
+  }
+  return out;
+}
 
 std::uint64_t host_hash() {
   char name[256] = {0};
@@ -919,6 +1267,12 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   mine.channelDomain = comm->channel_domain();
   mine.prefer = virtualHosts ? 1 : prefLocal;
   mine.fault = env_fault();
+  mine.relay = env_relay();
+  mine.stickBytes = bytes[0];
+  {
+    const char* rv = std::getenv("SPFFT_RELAY_VIRTUAL");
+    mine.relayVirtual = rv && *rv ? std::max(1, std::min(8, std::atoi(rv))) : 2;
+  }
   const int P = comm->size();
   std::vector<NodeInfo> all(P);
   comm->allgather(&mine, all.data(), sizeof(NodeInfo));
@@ -937,6 +1291,26 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   // every rank decides from rank 0's settings (environments may differ)
   const int prefer = all[0].prefer;
   const int fault = all[0].fault;
+  // relay routing through idle GPUs of the node (RelayDeviceComm): the buffered
+  // exchanges of ranks on distinct GPUs when other GPUs are idle (SPFFT_RELAY
+  // auto), or through virtual relays on the ranks' own GPUs (force, tests)
+  const int relayMode = all[0].relay;
+  if (oneNode && !unbuffered && fault == 0 && prefer == 0 && relayMode != 1 &&
+      (relayMode == 2 || !sharedDevice)) {
+    std::vector<int> relays;
+    if (relayMode == 2) {
+      relays.assign(all[0].relayVirtual, device);
+    } else {
+      std::vector<PciId> used;
+      for (int q = 0; q < P; ++q) used.push_back(PciId{all[q].domain, all[q].bus, all[q].device});
+      relays = idle_devices(*comm, used);
+    }
+    double perPeer = 0;
+    for (int q = 0; q < P; ++q) perPeer = std::max(perPeer, static_cast<double>(all[q].stickBytes) / P);
+    const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()));
+    if (!relays.empty() && pays)
+      return std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays));
+  }
   const bool peer =
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
   if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));

@@ -122,6 +122,11 @@ public:
   // plane leases exported memory from the IPC arena); null if the grid's own
   // buffer is used.
   virtual void* local_buffer(int /*slot*/) const { return nullptr; }
+  // Most exchange steps a direction should be cut into (0: any; host-
+  // synchronous planes that pay a host round trip per step want 1).
+  virtual int max_pipeline_steps() const { return 0; }
+  // Idle GPUs the plane relays through (RelayDeviceComm), 0 otherwise.
+  virtual int relay_count() const { return 0; }
   // Throws if an asynchronous failure (e.g. a barrier timeout) was recorded.
   virtual void check() {}
   // Failure detection while the host waits on a stream that carries exchanges:

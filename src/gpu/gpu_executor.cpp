@@ -146,7 +146,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     chunks = env_int("SPFFT_EXCH_CHUNKS", chunks, 1, 64);
     int blocks = perPeer >= 8.0 * (1 << 20) ? 2 : 1;
     blocks = env_int("SPFFT_EXCH_STICK_BLOCKS", blocks, 1, 16);
-    if (peerWrites_) chunks = blocks = 1;
+    if (peerWrites_ || grid_->device_comm().max_pipeline_steps() == 1) chunks = blocks = 1;
     // rank 0's counts; the chunk count reduced until the (padded) layout fits
     // every rank's buffers
     int req[3] = {chunks, 1, blocks};

@@ -285,3 +285,46 @@ def test_bench_ipc_unbuffered_few_hw_queues(gpu, monkeypatch, queues, barrier):
     # the transforms run on the 4 torch streams; the library owns only the peer
     # channel stream in channel mode
     assert cfg["library_streams"] == (1 if barrier == "channel" else 0), cfg
+
+
+# Relay routing (RelayDeviceComm): on an 8-GPU node with ranks on fewer GPUs, each
+# peer message is split between the direct xGMI link and two-hop routes through the
+# idle GPUs. On the one-GPU box, SPFFT_RELAY=force relays through virtual relay
+# buffers on the rank's own GPU: the same layouts, shares, two phases and barriers.
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc,exchange,relays", [(2, "COMPACT_BUFFERED", 2), (3, "BUFFERED_FLOAT", 3),
+                                                   (2, "BUFFERED", 1), (3, "COMPACT_BUFFERED_FLOAT", 2)])
+def test_torch_dist_relay_forced(gpu, monkeypatch, nproc, exchange, relays):
+    monkeypatch.setenv("SPFFT_RELAY", "force")
+    monkeypatch.setenv("SPFFT_RELAY_VIRTUAL", str(relays))
+    monkeypatch.setenv("SPFFT_RELAY_MIN_BYTES", "0")
+    _launch(nproc, exchange, "--iters=3", "--dims=48,40,36", expect="relay")
+
+
+@pytest.mark.gpu
+def test_fuzz_dist_relay_forced(gpu):
+    """The random distributions (empty ranks included) through the relay plane."""
+    code, out = _launch_tool(3, "fuzz_dist.py", "--cases", "30", "--seed", "12",
+                             env_extra={"SPFFT_RELAY": "force", "SPFFT_RELAY_MIN_BYTES": "0",
+                                        "SPFFT_RELAY_VIRTUAL": "2"})
+    assert code == 0, out[-4000:]
+    assert "30/30 passed" in out and "plane=relay" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_bench_relay_model(gpu, monkeypatch):
+    """bench.py over the forced relay plane: checked round trip on both ranks, and the
+    modelled link time accounts for the relay shares."""
+    monkeypatch.setenv("SPFFT_RELAY", "force")
+    monkeypatch.setenv("SPFFT_RELAY_VIRTUAL", "3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--size", "96", "--transforms", "2"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    cfg = _bench_json(r.stdout)["config"]
+    assert cfg["data_plane"] == "relay" and cfg["check_error"]["ok"], cfg
+    assert cfg["model_ms"]["relay_gpus"] == 3
