@@ -41,13 +41,21 @@ def build(clean: bool = False, jobs: int | None = None, build_type: str = "Relea
     _check_targets()
     os.makedirs(NATIVE_DIR, exist_ok=True)
     for so in glob.glob(os.path.join(BUILD_DIR, "libspfft_amd*.so")):
-        shutil.copy2(so, os.path.join(NATIVE_DIR, os.path.basename(so)))
+        _install(so, os.path.join(NATIVE_DIR, os.path.basename(so)))
     for exe in ("spfft_bench", "spfft_native_tests", "spfft_mpi_tests", "example_c",
                 "example_cpp", "example_f90"):
         src = os.path.join(BUILD_DIR, exe)
         if os.path.exists(src):
-            shutil.copy2(src, os.path.join(NATIVE_DIR, exe))
+            _install(src, os.path.join(NATIVE_DIR, exe))
     return NATIVE_DIR
+
+
+def _install(src, dst):
+    """Copy then rename: a process that has the old library mapped keeps its
+    (unlinked) file; copying over it in place would change the pages under it."""
+    tmp = dst + ".tmp"
+    shutil.copy2(src, tmp)
+    os.replace(tmp, dst)
 
 
 def _check_targets():

@@ -253,3 +253,26 @@ def test_default_exchange_is_compact():
         g = _dist_grid(comm, 8, 8, 8, 64, 4)
         return g.exchange_type
     assert run_ranks(2, body) == [sp.ExchangeType.COMPACT_BUFFERED] * 2
+
+
+def test_bench_model_relay_shares():
+    """bench.py's exchange model (config.model_ms): link time of a direct exchange,
+    and of the relay plane, whose shares cut every link's load to (N-1)/(N-1+K) in
+    two hops."""
+    import importlib.util
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(repo, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    stages = {"backward": {"z": 0.07, "y+x": 0.18, "exchange": 0.7, "total": 0.95},
+              "forward": {"x+y": 0.17, "z": 0.06, "exchange": 0.7, "total": 0.93}}
+    direct = b._model(stages, 52.7e6, 2, 1, 1)
+    relay = b._model(stages, 52.7e6, 2, 1, 1, relays=6)
+    assert abs(direct["backward"]["link_ms"] - 52.7e6 / 70e9 * 1e3) < 1e-9
+    assert abs(relay["backward"]["link_ms"] - 2 * direct["backward"]["link_ms"] / 7) < 1e-9
+    assert direct["backward"]["bound"] == "link" and relay["relay_gpus"] == 6
+    assert abs(direct["backward"]["compute_ms"] - 0.25) < 1e-12
+    # pipelined grid: all but one step's compute hidden behind the link
+    piped = b._model(stages, 52.7e6, 2, 2, 2)
+    assert abs(piped["backward"]["predicted_ms"] - (direct["backward"]["link_ms"] + 0.25 / 4)) < 1e-9

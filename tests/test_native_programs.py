@@ -143,3 +143,25 @@ def test_host_unbuffered_alltoallw_mpi(tmp_path, nranks):
     assert j["results"][0]["transforms_per_second"] > 0
     assert "alltoallw" in text
     assert "pack" not in text
+
+
+@pytest.mark.gpu
+def test_bench_cli_mpi_4ranks_shared_gpu(gpu, tmp_path):
+    """Four MPI ranks on the box's one GPU (the several-ranks-per-GPU layout of
+    plane-wave codes), every exchange type through the IPC peer-write plane, two
+    transforms per step: the C++ benchmark's rates (profiles/r5/ipc/)."""
+    import json
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("mpiexec not available")
+    out = tmp_path / "m4.json"
+    _run([MPIEXEC, "-n", "4", _prog("spfft_bench"), "-d", "128", "128", "128", "-r", "10", "-m", "2",
+          "-o", str(out), "-e", "all", "-p", "gpu-gpu", "--cutoff", "0.5"])
+    j = json.loads(out.read_text())
+    assert len(j["results"]) >= 3
+    assert all(r["transforms_per_second"] > 0 for r in j["results"])
+    # keep the record next to the profiles when asked (the GPU runs of the round)
+    keep = os.environ.get("SPFFT_KEEP_BENCH")
+    if keep:
+        os.makedirs(os.path.dirname(keep), exist_ok=True)
+        with open(keep, "w") as f:
+            f.write(out.read_text())
