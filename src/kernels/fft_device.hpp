@@ -149,9 +149,10 @@ struct CtShapeT<float, 1024> {
 // shape (E = 8, 256 threads per 8 lines) doubles the waves per SIMD that the
 // LDS budget allows, which the memory-bound stages turn into bandwidth:
 // measured on MI355X at 256^3 (profiles/r2_s1/shape_ab.txt) x backward 97.6 ->
-// 93.1 us, x/y forward -1 us. The row-mapped z stages keep E = 16 (one LDS
-// exchange instead of two): forward 65.7 vs 71.7 us with E = 8 (round 2),
-// backward 67.3 vs 68.0 us, 256^3 R2C 31.7 vs 34.2 us (profiles/r5/ab/c2r_twiddles).
+// 93.1 us, x/y forward -1 us. The row-mapped z backward also takes it: with
+// the twiddle powers (FftCT::kTwPow) 68.8-71.4 -> 62.0-62.3 us against E = 16
+// (profiles/r5/ab/f64b); the forward z stage keeps E = 16 (65.7 vs 71.7 us with
+// E = 8 in round 2).
 struct CtShape256E8 {
   static constexpr int E = 8, R0 = 8, R1 = 8, R2 = 4, kBudget = kLdsBudget;
 };
@@ -228,6 +229,12 @@ template <>
 struct CtShapeSel<double, 256, 1, true> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
+template <>
+struct CtShapeSel<double, 256, 1, false> : CtShape256E8 {};
+// (fp32 z backward likewise: 31.1 -> 28.9-29.3 us at 256^3; the z forward
+// stages are no faster with E = 8 in either precision, profiles/r5/ab/zf)
+template <>
+struct CtShapeSel<float, 256, 1, false> : CtShape256E8 {};
 
 // Twiddles of a pass: one table entry per butterfly group and its powers
 // formed in registers (twiddle_powers), unless the shape declares
