@@ -910,6 +910,60 @@ public:
     segsDev_.reset(new DeviceBuffer(maxSegs * sizeof(dev::CopySeg)));
     gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     comm_->barrier();
+    self_test();
+  }
+
+  // Collective. One exchange of a known pattern through every route (direct
+  // parts and relay shares) before the plane carries data; a wrong byte on any
+  // rank raises MPIError on every rank, and DeviceComm::create falls back to
+  // the RCCL plane. (The routes cross GPUs whose caches the one-GPU test box
+  // cannot exercise; a plane that does not deliver must not be used.)
+  void self_test() {
+    DeviceGuard guard(device_);
+    const std::size_t sideBytes = std::min(sides_[0] ? sides_[0]->bytes() : 0, sides_[1] ? sides_[1]->bytes() : 0);
+    long long per = static_cast<long long>(sideBytes / static_cast<std::size_t>(P_)) / 64 * 64;
+    per = std::min<long long>(per, 2LL << 20);
+    int ok = 1;
+    if (per >= 64) {
+      const int words = static_cast<int>(per / 8);
+      std::vector<unsigned long long> pattern(static_cast<std::size_t>(words) * P_);
+      auto word = [](int from, int to, int i) {
+        return (static_cast<unsigned long long>(from) << 48) ^ (static_cast<unsigned long long>(to) << 32) ^
+               static_cast<unsigned long long>(i) * 2654435761ull;
+      };
+      for (int q = 0; q < P_; ++q)
+        for (int i = 0; i < words; ++i) pattern[static_cast<std::size_t>(q) * words + i] = word(me_, q, i);
+      const char* fi = std::getenv("SPFFT_FAULT_RELAY_SELFTEST");
+      if (fi && *fi == '1' && me_ == P_ - 1 && P_ > 1) pattern[static_cast<std::size_t>((me_ + 1) % P_) * words] ^= 1;
+      void* send = sides_[0]->data();
+      void* recv = sides_[1]->data();
+      gpu_check(hipMemcpy(send, pattern.data(), pattern.size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
+      gpu_check(hipMemset(recv, 0, pattern.size() * 8), "hipMemset");
+      std::vector<std::int64_t> cnt(P_, per), dsp(P_);
+      for (int q = 0; q < P_; ++q) dsp[q] = static_cast<std::int64_t>(q) * per;
+      const long long saved = minBytes_;
+      minBytes_ = 0;  // every route, whatever the production threshold
+      alltoallv(send, cnt.data(), dsp.data(), recv, cnt.data(), dsp.data(), nullptr);
+      minBytes_ = saved;
+      gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      std::vector<unsigned long long> got(pattern.size());
+      gpu_check(hipMemcpy(got.data(), recv, got.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+      for (int q = 0; q < P_ && ok; ++q)
+        for (int i = 0; i < words; ++i)
+          if (got[static_cast<std::size_t>(q) * words + i] != word(q, me_, i)) {
+            ok = 0;
+            break;
+          }
+    }
+    std::vector<int> oks(P_);
+    comm_->allgather(&ok, oks.data(), sizeof(int));
+    for (int q = 0; q < P_; ++q)
+      if (!oks[q]) {
+        for (void* p : opened_) ipc_close(p);
+        opened_.clear();
+        set_error_detail("relay data plane: self-test exchange delivered wrong data to rank " + std::to_string(q));
+        throw MPIError();
+      }
   }
 
   ~RelayDeviceComm() override {
@@ -1308,8 +1362,15 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     double perPeer = 0;
     for (int q = 0; q < P; ++q) perPeer = std::max(perPeer, static_cast<double>(all[q].stickBytes) / P);
     const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()));
-    if (!relays.empty() && pays)
-      return std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays));
+    if (!relays.empty() && pays) {
+      try {
+        return std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays));
+      } catch (const MPIError&) {
+        // every rank agreed on the failure (setup or self-test): the next plane
+        if (comm->rank() == 0)
+          std::fprintf(stderr, "spfft: %s; not relaying\n", error_detail().c_str());
+      }
+    }
   }
   const bool peer =
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);

@@ -328,3 +328,16 @@ def test_bench_relay_model(gpu, monkeypatch):
     cfg = _bench_json(r.stdout)["config"]
     assert cfg["data_plane"] == "relay" and cfg["check_error"]["ok"], cfg
     assert cfg["model_ms"]["relay_gpus"] == 3
+
+
+@pytest.mark.gpu
+def test_relay_self_test_failure_falls_back(gpu, monkeypatch):
+    """The relay plane checks every route with a known pattern before it carries data;
+    a wrong byte on any rank (fault injection) makes every rank drop the relay plane
+    for the next one (here, ranks sharing the GPU: IPC peer writes), with the cause
+    printed once."""
+    monkeypatch.setenv("SPFFT_RELAY", "force")
+    monkeypatch.setenv("SPFFT_FAULT_RELAY_SELFTEST", "1")
+    code, out = _launch_tool(2, "rccl_probe.py", "COMPACT_BUFFERED", "--iters=2")
+    assert code == 0, out[-4000:]
+    assert out.count("[ipc]") == 2 and "self-test exchange delivered wrong data" in out, out[-4000:]
