@@ -1411,16 +1411,32 @@ __global__ void __launch_bounds__(Eng::kBlock)
     eng.lds_to_lds(lds, twh);
   }
   cx<T>* dst = inter + static_cast<long long>(zl) * a.interZStride + y0;
-  // post pass: lanes run over rows first, so the column stores are contiguous
-  for (int idx = threadIdx.x; idx < B * (h + 1); idx += blockDim.x) {
-    const int b = idx % B, k = idx / B;
-    const int c = xcol_of(a, xCol, k);
-    if (c < 0 || b >= yl) continue;
-    const cx<T> yk = lds[eng.out_at(b, k == h ? 0 : k)];
-    const cx<T> ym = conj(lds[eng.out_at(b, k == 0 ? 0 : h - k)]);
-    const cx<T> e = scale(yk + ym, T(0.5));
-    const cx<T> o = scale(rot<-1>(yk - ym), T(0.5));
-    st_inter(&dst[inter_row(a, c) + b], e + twm<-1>(o, twn[k]));
+  // post pass over the pairs (k, h - k), k <= h/2: both outputs need the same
+  // two LDS values, and w^(h-k) = -conj(w^k) (w = exp(-2 pi i / n), n = 2h), so
+  // a pair costs two LDS reads and one twiddle load instead of four and two
+  // (512^3 R2C fp32 x forward 224-226 -> 214-216 us, 256^3 R2C fp64 55 -> 53 us,
+  // profiles/r5/ab/r2cpair). Lanes run over rows first, so the column stores are
+  // contiguous.
+  for (int idx = threadIdx.x; idx < B * (h / 2 + 1); idx += blockDim.x) {
+    const int b = idx % B, k = idx / B, m = h - k;
+    if (b >= yl) continue;
+    const int ck = xcol_of(a, xCol, k), cm = xcol_of(a, xCol, m);
+    if (ck < 0 && cm < 0) continue;
+    const cx<T> A = lds[eng.out_at(b, k == h ? 0 : k)];
+    const cx<T> Bv = lds[eng.out_at(b, m == h ? 0 : m)];
+    const cx<T> wk = twn[k];
+    if (ck >= 0) {
+      const cx<T> ym = conj(Bv);
+      const cx<T> e = scale(A + ym, T(0.5));
+      const cx<T> o = scale(rot<-1>(A - ym), T(0.5));
+      st_inter(&dst[inter_row(a, ck) + b], e + twm<-1>(o, wk));
+    }
+    if (cm >= 0 && m != k) {
+      const cx<T> ym = conj(A);
+      const cx<T> e = scale(Bv + ym, T(0.5));
+      const cx<T> o = scale(rot<-1>(Bv - ym), T(0.5));
+      st_inter(&dst[inter_row(a, cm) + b], e + twm<-1>(o, mk<T>(-wk.x, wk.y)));
+    }
   }
 }
 
