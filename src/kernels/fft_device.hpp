@@ -234,6 +234,15 @@ template <>
 struct CtShapeSel<double, 256, -1, true> : CtShape256E8 {};
 template <>
 struct CtShapeSel<double, 256, 1, false> : CtShape256E8 {};
+// fp32 N = 512 z backward (row-mapped): 16 elements per lane, radices 16 x 16 x 2
+// (32 lanes per line). Measured on MI355X, same box (profiles/r5/ab/z512): 512^3
+// R2C z backward 145.9 -> 139.3 us; for the z forward it is slower (112 -> 133
+// us) and the 32-element shape slower in both (169 / 153 us).
+struct CtShapeZ512B {
+  static constexpr int E = 16, R0 = 16, R1 = 16, R2 = 2, kBudget = kLdsBudget;
+};
+template <>
+struct CtShapeSel<float, 512, 1, false> : CtShapeZ512B {};
 // (fp32 z backward likewise: 31.1 -> 28.9-29.3 us at 256^3; the z forward
 // stages are no faster with E = 8 in either precision, profiles/r5/ab/zf)
 template <>
