@@ -39,6 +39,9 @@ REF_FFT_ONLY_256_BY_T = {1: 2210.2, 4: 2418.3}  # profiles/r3/comparator/
 # 153.6 GB/s per link both directions, ~70 GB/s usable one way), the model's
 # assumption until the driver's N = 2/4/8 runs measure it
 LINK_GBPS = 70.0
+# host round trips of one relay-plane exchange (two stream synchronisations and the
+# node-local shared-memory collectives; profiles/r5/relay/overhead.txt)
+RELAY_HOST_MS = 0.06
 
 
 def _model(stages, sent_per_rank, world, chunks, blocks, relays=0):
@@ -54,8 +57,11 @@ def _model(stages, sent_per_rank, world, chunks, blocks, relays=0):
     # peer message, in two host-synchronous hops (push, pull)
     share = (world - 1) / (world - 1 + relays) if relays else 1.0
     link_ms = per_peer * share / (LINK_GBPS * 1e9) * 1e3 * (2 if relays else 1)
+    link_ms += RELAY_HOST_MS if relays else 0.0
     out = {"link_GBps_assumed": LINK_GBPS, "bytes_per_peer": per_peer,
            "chunks": chunks, "stick_blocks": blocks, "relay_gpus": relays}
+    if relays:
+        out["relay_host_ms"] = RELAY_HOST_MS
     for d in ("backward", "forward"):
         st = stages.get(d, {})
         compute = sum(v for k, v in st.items() if k not in ("exchange", "exchange-span", "exchange-tail", "total"))

@@ -80,6 +80,7 @@ def _prototypes(lib):
     sig["spfft_amd_comm_destroy"] = [V]
     sig["spfft_amd_comm_rank"] = [V, c_int_p]
     sig["spfft_amd_comm_size"] = [V, c_int_p]
+    sig["spfft_amd_comm_shm_check"] = [V, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     sig["spfft_amd_grid_create_distributed"] = [c_void_pp, I, I, I, I, I, I, I, V, I]
     sig["spfft_amd_float_grid_create_distributed"] = [c_void_pp, I, I, I, I, I, I, I, V, I]
     sig["spfft_amd_grid_exchange_type"] = [V, c_int_p]

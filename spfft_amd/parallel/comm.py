@@ -34,6 +34,15 @@ class Communicator:
         _check(lib().spfft_amd_comm_size(self.handle, ctypes.byref(v)))
         return v.value
 
+    def shm_check(self, iters: int = 200):
+        """Collective. Node-local shared-memory collectives (the relay data plane's host
+        synchronisation) against this communicator's own: microseconds per checked
+        allgather + barrier round, ``(shm_us, comm_us)``; ``shm_us`` is None when the
+        ranks cannot share a segment."""
+        shm, com = ctypes.c_double(), ctypes.c_double()
+        _check(lib().spfft_amd_comm_shm_check(self.handle, int(iters), ctypes.byref(shm), ctypes.byref(com)))
+        return (shm.value if shm.value >= 0 else None), com.value
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:

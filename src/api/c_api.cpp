@@ -1,12 +1,15 @@
 // C API (reference: extern "C" blocks of src/spfft/{grid,transform,multi_transform}[_float].cpp)
 // plus the SpFFT-AMD extensions of spfft/amd.h. Every entry point converts
 // exceptions into SpfftError codes; a null handle is SPFFT_INVALID_HANDLE_ERROR.
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "api/transform_impl.hpp"
 #include "comm/callback_comm.hpp"
+#include "comm/shm_group.hpp"
 #include "gpu/gpu_runtime.hpp"
 #include "core/common.hpp"
 #include "core/timing.hpp"
@@ -333,6 +336,38 @@ SpfftError spfft_amd_comm_rank(SpfftAmdComm comm, int* rank) {
 
 SpfftError spfft_amd_comm_size(SpfftAmdComm comm, int* size) {
   return with_handle<CommHandle>(comm, [&](CommHandle& c) { *size = c->size(); });
+}
+
+SpfftError spfft_amd_comm_shm_check(SpfftAmdComm comm, int iters, double* shmUs, double* commUs) {
+  if (!shmUs || !commUs || iters < 1) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<CommHandle>(comm, [&](CommHandle& c) {
+    Communicator& cm = *c;
+    const int P = cm.size(), me = cm.rank();
+    std::vector<long long> mine(4), all(static_cast<std::size_t>(4) * P);
+    auto round = [&](int it, auto&& gather, auto&& barrier) {
+      for (int k = 0; k < 4; ++k) mine[k] = (static_cast<long long>(it) << 20) + me * 4 + k;
+      gather(mine.data(), all.data(), mine.size() * sizeof(long long));
+      for (int q = 0; q < P; ++q)
+        for (int k = 0; k < 4; ++k)
+          if (all[static_cast<std::size_t>(q) * 4 + k] != (static_cast<long long>(it) << 20) + q * 4 + k) {
+            set_error_detail("shared-memory allgather delivered wrong data");
+            throw MPIError();
+          }
+      barrier();
+    };
+    auto timed = [&](auto&& gather, auto&& barrier) {
+      round(-1, gather, barrier);
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int it = 0; it < iters; ++it) round(it, gather, barrier);
+      return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+    };
+    auto shm = ShmGroup::create(cm, mine.size() * sizeof(long long), 60.0);
+    *shmUs = shm ? timed([&](const void* s, void* r, std::size_t n) { shm->allgather(s, r, n); },
+                         [&] { shm->barrier(); })
+                 : -1.0;
+    *commUs = timed([&](const void* s, void* r, std::size_t n) { cm.allgather(s, r, n); },
+                    [&] { cm.barrier(); });
+  });
 }
 
 SpfftError spfft_amd_grid_create_distributed(SpfftGrid* grid, int maxDimX, int maxDimY,

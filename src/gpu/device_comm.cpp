@@ -23,6 +23,7 @@
 #include "kernels/peer_sync.hpp"
 #include "kernels/relay_copy.hpp"
 #include "spfft/exceptions.hpp"
+#include "comm/shm_group.hpp"
 
 namespace spfft {
 
@@ -909,6 +910,9 @@ public:
     segsHost_.resize(maxSegs);
     segsDev_.reset(new DeviceBuffer(maxSegs * sizeof(dev::CopySeg)));
     gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    // the per-exchange host collectives (one allgather, two barriers) through
+    // shared memory when every rank maps the segment, else through comm
+    shm_ = ShmGroup::create(*comm_, sizeof(Transfer) * static_cast<std::size_t>(2 * P_ + 1), comm_timeout_seconds());
     comm_->barrier();
     self_test();
   }
@@ -992,7 +996,7 @@ public:
     if (static_cast<int>(xs.size()) > W) throw InternalError();
     std::copy(xs.begin(), xs.end(), wire.begin());
     std::vector<Transfer> all(static_cast<std::size_t>(W) * P_);
-    comm_->allgather(wire.data(), all.data(), sizeof(Transfer) * W);
+    host_allgather(wire.data(), all.data(), sizeof(Transfer) * W);
     // matched pairs p -> q: send offset, receive offset, bytes (NCCL matching
     // rule: one send and one receive per ordered pair in these lists)
     std::vector<long long> so(P_ * P_, -1), ro(P_ * P_, -1), nb(P_ * P_, 0);
@@ -1040,7 +1044,7 @@ public:
       run_segs(stream);
       gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     }
-    comm_->barrier();
+    host_barrier();
     // phase 2: pull the direct parts and the relayed shares addressed here
     segCount_ = 0;
     for (int p = 0; p < P_; ++p) {
@@ -1055,7 +1059,7 @@ public:
       run_segs(stream);
       gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     }
-    comm_->barrier();  // send sides and relay buffers are free again
+    host_barrier();  // send sides and relay buffers are free again
     sync_end(sync, stream);
   }
   int plane_rank() const override { return me_; }
@@ -1070,7 +1074,7 @@ public:
   std::string describe() const override {
     std::string d = "relay (" + std::to_string(P_) + " ranks, " + std::to_string(K_) + " relay GPU(s):";
     for (int c : relayDev_) d += " " + std::to_string(c);
-    return d + ")";
+    return d + (shm_ ? "; host sync: shared memory)" : "; host sync: communicator)");
   }
   int relay_count() const override { return K_; }
 
@@ -1079,6 +1083,18 @@ private:
   [[noreturn]] void mismatch() {
     set_error_detail("relay exchange: transfer lists of the ranks do not match");
     throw MPIError();
+  }
+  void host_barrier() {
+    if (shm_)
+      shm_->barrier();
+    else
+      comm_->barrier();
+  }
+  void host_allgather(const void* send, void* recv, std::size_t bytes) {
+    if (shm_)
+      shm_->allgather(send, recv, bytes);
+    else
+      comm_->allgather(send, recv, bytes);
   }
   void add_seg(const char* src, char* dst, long long bytes) {
     if (bytes <= 0) return;
@@ -1110,6 +1126,7 @@ private:
   std::vector<dev::CopySeg> segsHost_;
   std::size_t segCount_ = 0;
   std::unique_ptr<DeviceBuffer> segsDev_;
+  std::unique_ptr<ShmGroup> shm_;
 };
 
 struct NodeInfo {
@@ -1126,13 +1143,15 @@ struct NodeInfo {
 
 // SPFFT_RELAY=auto: whether relaying through K idle GPUs beats the direct
 // links for per-peer messages of m bytes among n ranks. Direct: m at one link's
-// rate; relay: two hops of (n - 1) / (n - 1 + K) of m each, plus ~100 us of
-// host round trips (two stream synchronisations, two barriers). Relay is
-// chosen when it models at least 20% faster: N = 2 at 256^3 fp64 (52 MB per
-// peer, K = 6: 750 vs 315 us) relays; N = 4 (13 MB, K = 4: 190 vs 260 us)
-// and small problems stay on RCCL.
+// rate; relay: two hops of (n - 1) / (n - 1 + K) of m each, plus ~60 us of
+// host round trips (two stream synchronisations, the node-local shared-memory
+// allgather and barriers: 42-53 us per exchange measured with 2 ranks on one
+// MI355X, 220-280 us through the gloo control plane; profiles/r5/relay/
+// overhead.txt). Relay is chosen when it models at least 20% faster: N = 2 at
+// 256^3 fp64 (52 MB per peer, K = 6: 750 vs 275 us) relays; N = 4 (13 MB,
+// K = 4: 190 vs 220 us) and small problems stay on RCCL.
 bool relay_pays(double m, int n, int k) {
-  constexpr double kLinkBytesPerUs = 70e3, kHostUs = 100.0;
+  constexpr double kLinkBytesPerUs = 70e3, kHostUs = 60.0;
   const double direct = m / kLinkBytesPerUs;
   const double relay = 2.0 * m * (n - 1) / (n - 1 + k) / kLinkBytesPerUs + kHostUs;
   return relay < 0.8 * direct;

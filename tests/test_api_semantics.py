@@ -270,7 +270,7 @@ def test_bench_model_relay_shares():
     direct = b._model(stages, 52.7e6, 2, 1, 1)
     relay = b._model(stages, 52.7e6, 2, 1, 1, relays=6)
     assert abs(direct["backward"]["link_ms"] - 52.7e6 / 70e9 * 1e3) < 1e-9
-    assert abs(relay["backward"]["link_ms"] - 2 * direct["backward"]["link_ms"] / 7) < 1e-9
+    assert abs(relay["backward"]["link_ms"] - 2 * direct["backward"]["link_ms"] / 7 - b.RELAY_HOST_MS) < 1e-9
     assert direct["backward"]["bound"] == "link" and relay["relay_gpus"] == 6
     assert abs(direct["backward"]["compute_ms"] - 0.25) < 1e-12
     # pipelined grid: all but one step's compute hidden behind the link

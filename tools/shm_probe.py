@@ -1,0 +1,30 @@
+"""Node-local shared-memory collectives (the relay data plane's host synchronisation)
+against the torch.distributed gloo control plane, one OS process per rank:
+    python -m torch.distributed.run --standalone --local-addr=127.0.0.1 --nproc-per-node=3 \
+        tools/shm_probe.py [--iters N]
+Prints one line per rank: "SHM OK rank=r shm_us=... comm_us=...".
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=300)
+    args = ap.parse_args()
+    import torch.distributed as dist
+    from spfft_amd.parallel.comm import TorchDistComm
+
+    dist.init_process_group("gloo")
+    comm = TorchDistComm()
+    shm, com = comm.shm_check(args.iters)
+    print(f"SHM OK rank={dist.get_rank()} " + json.dumps({"shm_us": shm, "comm_us": com}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
