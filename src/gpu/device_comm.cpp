@@ -988,9 +988,10 @@ public:
     // the grid's exchange sides only
     if (recvSlot < 0 || send != local_buffer(sendSlot)) throw InternalError();
     sync_begin(sync, stream);
-    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     // every rank's transfer list (fixed size: own block + one send and one
-    // receive per peer)
+    // receive per peer); the host collective overlaps the GPU work still
+    // queued ahead of the exchange (the stream is synchronised before the
+    // barrier that lets peers read this rank's send side)
     const int W = 2 * P_ + 1;
     std::vector<Transfer> wire(W, Transfer{-1, 0, 0, 0, 0});
     if (static_cast<int>(xs.size()) > W) throw InternalError();
@@ -1040,10 +1041,8 @@ public:
       for (int c = 0; c < K_; ++c)
         add_seg(s + so[k] + direct + c * base[k], peers_[me_][2 + c] + roff[k], base[k]);
     }
-    if (segCount_ > 0) {
-      run_segs(stream);
-      gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-    }
+    run_segs(stream);
+    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     host_barrier();
     // phase 2: pull the direct parts and the relayed shares addressed here
     segCount_ = 0;
@@ -1108,6 +1107,12 @@ private:
       chunks += (static_cast<long long>(segsHost_[i].bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
     }
     if (segCount_ == 0) return;
+    if (segCount_ <= static_cast<std::size_t>(dev::kInlineSegs)) {
+      // the table travels in the kernel arguments (no host-to-device copy)
+      std::copy(segsHost_.begin(), segsHost_.begin() + static_cast<std::ptrdiff_t>(segCount_), inlineSegs_.s);
+      dev::launch_multi_copy_inline(inlineSegs_, static_cast<int>(segCount_), chunks, stream);
+      return;
+    }
     gpu_check(hipMemcpyAsync(segsDev_->data(), segsHost_.data(), segCount_ * sizeof(dev::CopySeg),
                              hipMemcpyHostToDevice, stream),
               "hipMemcpyAsync");
@@ -1127,6 +1132,7 @@ private:
   std::size_t segCount_ = 0;
   std::unique_ptr<DeviceBuffer> segsDev_;
   std::unique_ptr<ShmGroup> shm_;
+  dev::SegPack inlineSegs_{};
 };
 
 struct NodeInfo {

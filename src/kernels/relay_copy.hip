@@ -13,6 +13,7 @@
 
 #include "gpu/gpu_runtime.hpp"
 #include "kernels/relay_copy.hpp"
+#include "spfft/exceptions.hpp"
 
 namespace spfft {
 namespace dev {
@@ -20,7 +21,8 @@ namespace dev {
 namespace {
 constexpr int kCopyThreads = 256;
 
-__device__ __forceinline__ int find_seg(const CopySeg* __restrict__ s, int n, long long chunk) {
+template <class Segs>
+__device__ __forceinline__ int find_seg(const Segs& s, int n, long long chunk) {
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -33,8 +35,8 @@ __device__ __forceinline__ int find_seg(const CopySeg* __restrict__ s, int n, lo
 }
 }  // namespace
 
-__global__ void __launch_bounds__(kCopyThreads)
-    multi_copy_kernel(const CopySeg* __restrict__ segs, int nseg, long long totalChunks) {
+template <class Segs>
+__device__ __forceinline__ void multi_copy(const Segs& segs, int nseg, long long totalChunks) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (long long c = blockIdx.x; c < totalChunks; c += gridDim.x) {
@@ -62,12 +64,31 @@ __global__ void __launch_bounds__(kCopyThreads)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+__global__ void __launch_bounds__(kCopyThreads)
+    multi_copy_kernel(const CopySeg* __restrict__ segs, int nseg, long long totalChunks) {
+  multi_copy(segs, nseg, totalChunks);
+}
+
+__global__ void __launch_bounds__(kCopyThreads)
+    multi_copy_inline_kernel(const SegPack segs, int nseg, long long totalChunks) {
+  multi_copy(segs.s, nseg, totalChunks);
+}
+
 void launch_multi_copy(const CopySeg* devSegs, int nseg, long long totalChunks, hipStream_t stream) {
   if (nseg <= 0 || totalChunks <= 0) return;
   const long long grid = totalChunks < 2048 ? totalChunks : 2048;
   hipLaunchKernelGGL(multi_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCopyThreads), 0, stream,
                      devSegs, nseg, totalChunks);
   gpu_check_launch("multi_copy", stream);
+}
+
+void launch_multi_copy_inline(const SegPack& segs, int nseg, long long totalChunks, hipStream_t stream) {
+  if (nseg <= 0 || totalChunks <= 0) return;
+  if (nseg > kInlineSegs) throw InternalError();
+  const long long grid = totalChunks < 2048 ? totalChunks : 2048;
+  hipLaunchKernelGGL(multi_copy_inline_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCopyThreads), 0, stream,
+                     segs, nseg, totalChunks);
+  gpu_check_launch("multi_copy_inline", stream);
 }
 
 }  // namespace dev

@@ -22,5 +22,13 @@ struct CopySeg {
 // chunks in all) in one launch on `stream`.
 void launch_multi_copy(const CopySeg* devSegs, int nseg, long long totalChunks, hipStream_t stream);
 
+// Segments passed by value in the kernel arguments (at most kInlineSegs): no
+// host-to-device copy of the table ahead of the launch.
+constexpr int kInlineSegs = 96;
+struct SegPack {
+  CopySeg s[kInlineSegs];
+};
+void launch_multi_copy_inline(const SegPack& segs, int nseg, long long totalChunks, hipStream_t stream);
+
 }  // namespace dev
 }  // namespace spfft
