@@ -271,14 +271,60 @@ __device__ __forceinline__ void long_cols_body(const Eng& eng, const PassArgs& a
   }
   __syncthreads();
   eng.lds_to_lds(lds, tw1);
-  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-    const int b = idx % B, k1 = idx / B, j2 = j20 + (b >> ltShift);
-    const long long line = l0 + (b & (lt - 1));
-    if (j2 < a.n2 && line < a.lines) {
-      const cx<T> w = twM[static_cast<long long>(j2) * k1];
-      const cx<T> v = lds[eng.out_at(b, k1)];
-      work[line * a.stride + static_cast<long long>(k1) * a.n2 + j2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
+  // compile-time engines: a lane keeps its column j2 and walks k1 = k1f + m *
+  // step (m < kIt), so its twiddles w^(j2 k1) are one table entry per group of
+  // kG times the powers of w^(j2 step) formed in registers (twiddle_powers:
+  // a few ulp), instead of one table load per element from the n1 n2-entry
+  // table: those loads cost 305 -> 211 us of the 8192 x 64 x 64 fp64 forward
+  // columns pass (all loads removed, profiles/r5/long)
+  constexpr int kIt = [] {
+    if constexpr (Eng::kBatchedCopy) {
+      return 0;
+    } else {
+      constexpr int work = Eng::F::B * Eng::kN;
+      return work % Eng::F::NT == 0 ? work / Eng::F::NT : 0;
     }
+  }();
+  auto generic = [&] {
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int b = idx % B, k1 = idx / B, j2 = j20 + (b >> ltShift);
+      const long long line = l0 + (b & (lt - 1));
+      if (j2 < a.n2 && line < a.lines) {
+        const cx<T> w = twM[static_cast<long long>(j2) * k1];
+        const cx<T> v = lds[eng.out_at(b, k1)];
+        work[line * a.stride + static_cast<long long>(k1) * a.n2 + j2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
+      }
+    }
+  };
+  if constexpr (kIt >= 1) {
+    // (launched with the engine's own thread count, four_step)
+    if (blockDim.x != static_cast<unsigned>(Eng::F::NT)) {
+      generic();
+      return;
+    }
+    constexpr int kG = kIt < 8 ? kIt : 8;
+    const int b = static_cast<int>(threadIdx.x) % B, j2 = j20 + (b >> ltShift);
+    const long long line = l0 + (b & (lt - 1));
+    const int step = static_cast<int>(blockDim.x) / B, k1f = static_cast<int>(threadIdx.x) / B;
+    if (j2 < a.n2 && line < a.lines) {
+      cx<T> pw[kG > 1 ? kG - 1 : 1];
+      if constexpr (kG > 1) twiddle_powers<kG>(twM[static_cast<long long>(j2) * step], pw);
+      cx<T>* dstLine = work + line * a.stride + j2;
+#pragma unroll
+      for (int g = 0; g < kIt / kG; ++g) {
+        const int kg = k1f + g * kG * step;
+        const cx<T> wb = twM[static_cast<long long>(j2) * kg];
+#pragma unroll
+        for (int r = 0; r < kG; ++r) {
+          const int k1 = kg + r * step;
+          const cx<T> w = r == 0 ? wb : cmul(wb, pw[r > 0 ? r - 1 : 0]);
+          const cx<T> v = lds[eng.out_at(b, k1)];
+          dstLine[static_cast<long long>(k1) * a.n2] = S > 0 ? twm<+1>(v, w) : twm<-1>(v, w);
+        }
+      }
+    }
+  } else {
+    generic();
   }
 }
 template <class Eng, typename T, typename BT, int S>
