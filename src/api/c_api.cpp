@@ -2,6 +2,7 @@
 // plus the SpFFT-AMD extensions of spfft/amd.h. Every entry point converts
 // exceptions into SpfftError codes; a null handle is SPFFT_INVALID_HANDLE_ERROR.
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -362,6 +363,10 @@ SpfftError spfft_amd_comm_shm_check(SpfftAmdComm comm, int iters, double* shmUs,
       return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
     };
     auto shm = ShmGroup::create(cm, mine.size() * sizeof(long long), 60.0);
+    // fault injection (tests): the last rank leaves without a word; the others'
+    // shared-memory waits must end with MPIError, not spin
+    const char* fi = std::getenv("SPFFT_FAULT_SHM_EXIT");
+    if (shm && fi && *fi == '1' && me == P - 1 && P > 1) std::_Exit(0);
     *shmUs = shm ? timed([&](const void* s, void* r, std::size_t n) { shm->allgather(s, r, n); },
                          [&] { shm->barrier(); })
                  : -1.0;

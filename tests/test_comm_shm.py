@@ -49,3 +49,14 @@ def test_shm_segment_unlinked():
     _probe(2)
     after = set(n for n in os.listdir("/dev/shm") if n.startswith("spfft-"))
     assert after <= before, after - before
+
+
+def test_shm_peer_exit_detected():
+    """A rank that leaves while the others wait in a shared-memory barrier: the
+    waits end with an error naming the exited rank (liveness check), not a hang."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           "--nproc-per-node=2", os.path.join(REPO, "tools", "shm_probe.py"), "--iters", "300"]
+    e = dict(os.environ, OMP_NUM_THREADS="1", SPFFT_FAULT_SHM_EXIT="1")
+    r = subprocess.run(cmd, cwd=REPO, env=e, capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert "SHM ERROR rank=0" in out and "has exited" in out, out[-4000:]

@@ -21,7 +21,12 @@ def main():
 
     dist.init_process_group("gloo")
     comm = TorchDistComm()
-    shm, com = comm.shm_check(args.iters)
+    try:
+        shm, com = comm.shm_check(args.iters)
+    except Exception as e:  # noqa: BLE001
+        # (SPFFT_FAULT_SHM_EXIT: a peer left; the wait must end with an error)
+        print(f"SHM ERROR rank={dist.get_rank()} {e}", flush=True)
+        os._exit(0)
     print(f"SHM OK rank={dist.get_rank()} " + json.dumps({"shm_us": shm, "comm_us": com}), flush=True)
     dist.destroy_process_group()
 
