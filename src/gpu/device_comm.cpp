@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -529,6 +530,22 @@ std::shared_ptr<PeerChannel> acquire_peer_channel(const std::string& key, int de
   return ch;
 }
 
+// A failed route self-test of the peer-write plane (every rank throws it).
+struct PeerSelfTestFailed : MPIError {};
+
+unsigned long long fresh_test_nonce() {
+  std::random_device rd;
+  const auto t = static_cast<unsigned long long>(std::chrono::steady_clock::now().time_since_epoch().count());
+  return ((static_cast<unsigned long long>(rd()) << 32) ^ rd() ^ t ^ static_cast<unsigned long long>(getpid())) | 1ull;
+}
+
+// Fault injection (tests): the last rank corrupts one word of its message to
+// rank 0 in the peer plane's self-test.
+bool fault_flag_peer_selftest() {
+  const char* e = std::getenv("SPFFT_FAULT_PEER_SELFTEST");
+  return e && *e == '1';
+}
+
 class PeerDeviceComm : public DeviceComm {
 public:
   // In-process group (ipc == false): `buffers` are the grid's exchange sides,
@@ -549,11 +566,19 @@ public:
     peers_.assign(P_, {nullptr, nullptr, nullptr});
     const std::size_t fbytes = static_cast<std::size_t>(dev::peer_flag_words(std::max(P_, 1))) * 8;
     if (ipc_) {
+      xcdMask_ = dev::xcd_mask(device);
       open_ipc(bytes, fbytes);
       mode_ = peer_barrier_mode();
       if (mode_ == PeerBarrier::kChannel) channel_ = acquire_peer_channel(channelKey, device);
       if (mode_ == PeerBarrier::kStream)
         gpu_check(hipEventCreateWithFlags(&orderEv_, hipEventDisableTiming), "hipEventCreateWithFlags");
+      int rateKHz = 0;
+      gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, device),
+                "hipDeviceGetAttribute");
+      timeoutTicks_ = static_cast<long long>(peer_timeout_seconds() * 1e3 * std::max(rateKHz, 1));
+      comm_->barrier();  // every flag array is zeroed before the first barrier round
+      self_test();
+      return;
     } else {
       // in-process groups meet on the host: ranks of one process share its few
       // hardware queues, so a spinning barrier kernel could sit in front of
@@ -574,14 +599,8 @@ public:
         }
       }
     }
-    int rateKHz = 0;
-    gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, device),
-              "hipDeviceGetAttribute");
-    const char* env = std::getenv("SPFFT_PEER_TIMEOUT");
-    const double seconds = env && *env ? std::max(0.1, std::atof(env)) : 30.0;
-    timeoutTicks_ = static_cast<long long>(seconds * 1e3 * std::max(rateKHz, 1));
     gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    comm_->barrier();  // every flag array is zeroed before the first barrier round
+    comm_->barrier();
   }
 
   ~PeerDeviceComm() override {
@@ -638,6 +657,9 @@ public:
         *detail = "peer exchange: aborted (host-side timeout or an earlier failure)";
       else if (f & kTimedOut)
         *detail = "peer exchange: a rank did not reach the exchange barrier within SPFFT_PEER_TIMEOUT";
+      else if (f & dev::kPeerXcdMiss)
+        *detail = "peer exchange: a barrier round's workgroups did not run on every XCD (its L2 write-back "
+                  "would have missed one); nothing was published";
       else if (f & kPeerGaveUp)
         *detail = "peer exchange: a peer rank gave up waiting at the exchange barrier";
       else
@@ -658,7 +680,7 @@ public:
                         : mode_ == PeerBarrier::kChannel ? "peer channel" : "host";
     std::snprintf(b, sizeof(b), "ipc (%d ranks, barrier on %s; arena: %lld blocks allocated, %lld reused, %lld freed)",
                   P_, where, s.allocated, s.reused, s.freed);
-    return b;
+    return std::string(b) + "; self-test " + selfTest_;
   }
 
 private:
@@ -744,6 +766,89 @@ private:
               "hipMemcpy");
   }
 
+  static double peer_timeout_seconds() {
+    const char* env = std::getenv("SPFFT_PEER_TIMEOUT");
+    return env && *env ? std::max(0.1, std::atof(env)) : 30.0;
+  }
+
+  // Route self-test (the relay plane's, for the peer-write path): one exchange
+  // of a known pattern through the real path. Every rank fills its receive
+  // region with old contents and reads it from every XCD (stale L2 lines are
+  // the hazard of remote stores), meets the others on the host, stores the
+  // pattern into every peer's side with the stage kernels' store flavour, runs
+  // one barrier round, and checks every word it received. Every rank learns
+  // every outcome; any wrong word fails the plane on every rank
+  // (PeerSelfTestFailed: DeviceComm::create falls back to RCCL where it can).
+  void self_test() {
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Side {
+      unsigned long long bytes[2];
+      unsigned long long nonce;
+    };
+    Side mine{{sides_[0] ? static_cast<unsigned long long>(sides_[0]->bytes()) : 0ull,
+               sides_[1] ? static_cast<unsigned long long>(sides_[1]->bytes()) : 0ull},
+              fresh_test_nonce()};
+    std::vector<Side> all(P_);
+    comm_->allgather(&mine, all.data(), sizeof(Side));
+    unsigned long long minb[2] = {~0ull, ~0ull};
+    for (const Side& q : all)
+      for (int i = 0; i < 2; ++i) minb[i] = std::min(minb[i], q.bytes[i]);
+    const unsigned long long nonce = all[0].nonce;
+    // the slab side (the z stage's remote stores) when every rank has room
+    int slot = minb[1] / P_ >= 16 ? 1 : (minb[0] / P_ >= 16 ? 0 : -1);
+    if (slot < 0 || P_ < 2) {
+      selfTest_ = "skipped (an exchange side too small)";
+      return;
+    }
+    const std::size_t per = std::min<unsigned long long>(minb[slot] / P_, 256ull << 10) / 16 * 16;
+    DeviceGuard guard(device_);
+    GpuStream st(false);
+    DeviceBuffer words(2 * sizeof(unsigned long long));
+    unsigned long long* bad = words.data<unsigned long long>();
+    char* region = static_cast<char*>(peers_[me_][slot]);
+    gpu_check(hipMemsetAsync(bad, 0, 2 * sizeof(unsigned long long), st.get()), "hipMemsetAsync");
+    gpu_check(hipMemsetAsync(region, 0xA5, per * P_, st.get()), "hipMemsetAsync");
+    dev::launch_selftest_warm(region, per * P_, bad + 1, st.get());
+    gpu_check(hipStreamSynchronize(st.get()), "hipStreamSynchronize");
+    comm_->barrier();  // every receiver's L2 holds the old contents before any store
+    const int corrupt = fault_flag_peer_selftest() && me_ == P_ - 1 ? 1 : 0;
+    for (int k = 1; k < P_; ++k) {
+      const int q = (me_ + k) % P_;
+      dev::launch_selftest_store(static_cast<char*>(peers_[q][slot]) + me_ * per, per, nonce, me_, q,
+                                 corrupt && q == 0, st.get());
+    }
+    barrier(st.get());
+    for (int q = 0; q < P_; ++q)
+      if (q != me_) dev::launch_selftest_check(region + q * per, per, nonce, q, me_, bad, st.get());
+    unsigned long long wrong = 0;
+    gpu_check(hipMemcpyAsync(&wrong, bad, sizeof(wrong), hipMemcpyDeviceToHost, st.get()), "hipMemcpyAsync");
+    gpu_check(hipStreamSynchronize(st.get()), "hipStreamSynchronize");
+    lastStream_ = nullptr;
+    std::string d;
+    const int ok = healthy(&d) ? 1 : 0;
+    struct Res {
+      unsigned long long wrong;
+      int ok;
+    };
+    Res r{wrong, ok};
+    std::vector<Res> res(P_);
+    comm_->allgather(&r, res.data(), sizeof(Res));
+    const double ms = 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    char b[256];
+    for (int q = 0; q < P_; ++q) {
+      if (res[q].wrong == 0 && res[q].ok) continue;
+      std::snprintf(b, sizeof(b),
+                    "peer-write plane route self-test failed: rank %d received %llu wrong words of %zu-byte "
+                    "messages%s",
+                    q, res[q].wrong, per, res[q].ok ? "" : " (barrier failure)");
+      set_error_detail(b);
+      throw PeerSelfTestFailed();
+    }
+    std::snprintf(b, sizeof(b), "ok (%d ranks x %zu KiB, slot %d, %.2f ms)", P_, per >> 10, slot, ms);
+    selfTest_ = b;
+    selfTestMs_ = ms;
+  }
+
   void barrier(hipStream_t stream) {
     SPFFT_TIMED_SCOPE("peer_barrier");
     if (__atomic_load_n(failHost_, __ATOMIC_ACQUIRE) != 0) check();
@@ -755,14 +860,14 @@ private:
       hipStream_t cs = channel_->stream->get();
       gpu_check(hipEventRecord(channel_->in, stream), "hipEventRecord");
       gpu_check(hipStreamWaitEvent(cs, channel_->in, 0), "hipStreamWaitEvent");
-      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, cs);
+      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, xcdMask_, cs);
       gpu_check(hipEventRecord(channel_->out, cs), "hipEventRecord");
       gpu_check(hipStreamWaitEvent(stream, channel_->out, 0), "hipStreamWaitEvent");
     } else if (mode_ == PeerBarrier::kStream) {
       // rounds of this plane in issue order across streams
       if (lastStream_ != stream && epoch_ > 0)
         gpu_check(hipStreamWaitEvent(stream, orderEv_, 0), "hipStreamWaitEvent");
-      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, stream);
+      dev::launch_peer_barrier(table, mine, me_, P_, ++epoch_, failDev_, timeoutTicks_, xcdMask_, stream);
       gpu_check(hipEventRecord(orderEv_, stream), "hipEventRecord");
       lastStream_ = stream;
     } else {
@@ -788,7 +893,10 @@ private:
   hipStream_t lastStream_ = nullptr;
   unsigned long long epoch_ = 0;
   long long timeoutTicks_ = 0;
+  unsigned xcdMask_ = 0;
   bool readPending_[2] = {false, false};
+  std::string selfTest_ = "not run";
+  double selfTestMs_ = 0;
 };
 
 // ------------------------------------------------------------ relay routing
@@ -829,11 +937,28 @@ public:
         K_(static_cast<int>(relayDevices.size())), relayDev_(relayDevices) {
     DeviceGuard guard(device);
     const char* e = std::getenv("SPFFT_RELAY_MIN_BYTES");
-    minBytes_ = e && *e ? static_cast<long long>(std::atof(e)) : (1LL << 20);
     // relay capacity per idle GPU: a rank's relayed bytes per relay are at
     // most its send side / (N - 1 + K)
     const std::size_t side = std::max(bytes[0], bytes[1]);
     relayCap_ = side / static_cast<std::size_t>(std::max(1, P_ - 1 + K_)) + 4096;
+    // Every rank splits every sender's messages (exchange()), so each sender's
+    // capacity and the size threshold must be known everywhere: the caps are
+    // allgathered (side sizes differ per rank under COMPACT_BUFFERED) and the
+    // threshold is rank 0's. Side sizes feed the self-test's message size.
+    struct Setup {
+      unsigned long long cap, sides[2];
+      long long minBytes;
+    };
+    Setup su{relayCap_, {bytes[0], bytes[1]}, e && *e ? static_cast<long long>(std::atof(e)) : (1LL << 20)};
+    std::vector<Setup> sus(P_);
+    comm_->allgather(&su, sus.data(), sizeof(Setup));
+    minBytes_ = sus[0].minBytes;
+    capOf_.resize(P_);
+    minSide_ = ~0ull;
+    for (int q = 0; q < P_; ++q) {
+      capOf_[q] = static_cast<long long>(sus[q].cap);
+      minSide_ = std::min<unsigned long long>(minSide_, std::min(sus[q].sides[0], sus[q].sides[1]));
+    }
     struct Announce {
       IpcExport e[2 + kMaxRelays];
     };
@@ -924,8 +1049,9 @@ public:
   // cannot exercise; a plane that does not deliver must not be used.)
   void self_test() {
     DeviceGuard guard(device_);
-    const std::size_t sideBytes = std::min(sides_[0] ? sides_[0]->bytes() : 0, sides_[1] ? sides_[1]->bytes() : 0);
-    long long per = static_cast<long long>(sideBytes / static_cast<std::size_t>(P_)) / 64 * 64;
+    // the same message size on every rank (the smallest side of the group), so
+    // every rank makes the same collective calls with matching counts
+    long long per = static_cast<long long>(minSide_ / static_cast<unsigned long long>(P_)) / 64 * 64;
     per = std::min<long long>(per, 2LL << 20);
     int ok = 1;
     if (per >= 64) {
@@ -1019,7 +1145,7 @@ public:
         const long long m = nb[p * P_ + q];
         long long b = 0;
         if (q != p && K_ > 0 && m >= minBytes_) b = (m / (P_ - 1 + K_)) / 16 * 16;
-        if (used + b > static_cast<long long>(relayCap_)) b = 0;
+        if (used + b > capOf_[p]) b = 0;  // sender p's relay buffers
         base[p * P_ + q] = b;
         roff[p * P_ + q] = used;
         used += b;
@@ -1124,6 +1250,8 @@ private:
   std::vector<int> relayDev_;
   long long minBytes_ = 0;
   std::size_t relayCap_ = 0;
+  std::vector<long long> capOf_;     // every rank's relay capacity (per relay buffer)
+  unsigned long long minSide_ = 0;   // smallest exchange side of the group
   std::unique_ptr<IpcLease> sides_[2];
   std::vector<std::unique_ptr<IpcLease>> relay_;
   std::vector<std::vector<char*>> peers_;  // [rank][0: stick side, 1: slab side, 2 + c: relay c]
@@ -1399,7 +1527,17 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   }
   const bool peer =
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
-  if (peer) return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
+  if (peer) {
+    try {
+      return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
+    } catch (const PeerSelfTestFailed&) {
+      // every rank saw the failure: ranks on distinct devices move the data
+      // through RCCL instead (UNBUFFERED included); ranks sharing a device
+      // have no other plane (RCCL refuses them)
+      if (sharedDevice || !oneNode || prefer == 2) throw;
+      if (comm->rank() == 0) std::fprintf(stderr, "spfft: %s; using RCCL\n", error_detail().c_str());
+    }
+  }
   auto ch = acquire_channel(comm.get(), key, device, comm->rank(), P, false, fault);
   // every rank learns whether every RCCL communicator came up
   int ok = ch->ok() ? 1 : 0;

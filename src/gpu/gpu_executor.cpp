@@ -17,6 +17,20 @@
 namespace spfft {
 
 namespace {
+// A/B switch (profiles/r6/shared_gpu): 1 = every wave of a stage kernel that
+// stores into peers' memory ends with a system-scope release (the round-5
+// form); 0 (default) = the barrier round's per-XCD write-back publishes them.
+int stage_release_fence() {
+  static const int v = [] {
+    const char* e = std::getenv("SPFFT_STAGE_RELEASE");
+    return e && *e == '1' ? 1 : 0;
+  }();
+  return v;
+}
+}  // namespace
+
+
+namespace {
 int env_int(const char* name, int dflt, int lo, int hi) {
   const char* e = std::getenv(name);
   if (!e || !*e) return dflt;
@@ -904,7 +918,7 @@ void GpuExecutor<T>::backward_z(const T* input) {
     // the z stage stores straight into the peers' slab sides
     grid_->device_comm().prepare_write(GridImpl<T>::kSlabSide, stream_);
     a.zTab = zTabRemote_->data<long long>();
-    a.remote = 1;
+    a.remote = stage_release_fence();
   }
   // pipelined plans: one launch per stick block, whose messages leave as soon
   // as it is done (zEv_, run_steps)
@@ -1151,7 +1165,7 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       } else if (peerWrites_) {
         ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
         set_col_desc(ya, colDescRemote_);
-        ya.remote = 1;
+        ya.remote = stage_release_fence();
       }
       cx<T>* out = inter_for(inter, z0);
       x_forward_launch(xa, space, out);

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--only", type=int, default=-1, help="run only this case (the draws of the others still happen)")
     ap.add_argument("--teardown", choices=["lazy", "collective"], default="lazy",
                     help="collective: drop each case's grid on every rank, then barrier, before the next case")
+    ap.add_argument("--maxima", choices=["global", "local"], default="global",
+                    help="local: every rank passes its own stick count and plane count as the "
+                         "grid maxima (zero on empty ranks), so exchange sides differ per rank")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -83,7 +86,8 @@ def main():
         vals = dense_forward(field, all_idx, dims, r2c=r2c)
         ref = dense_backward(all_idx, vals, dims, r2c=r2c)
         starts = np.concatenate([[0], np.cumsum([len(p) for p in parts])])
-        ms = max(len(np.unique(p[:, 0].astype(np.int64) * ny + p[:, 1])) if len(p) else 0 for p in parts)
+        sticks = [len(np.unique(p[:, 0].astype(np.int64) * ny + p[:, 1])) if len(p) else 0 for p in parts]
+        ms = max(sticks)
         tol = 2e-4 if (single or exchange.endswith("FLOAT")) else 1e-10
         if a.only >= 0 and c != a.only:
             continue
@@ -92,7 +96,11 @@ def main():
         eb = ef = 0.0
         try:
             G = sp.GridFloat if single else sp.Grid
-            grid = G(nx, ny, nz, max(1, ms), PU, 1, max_local_z_length=max(planes), comm=TorchDistComm(),
+            if a.maxima == "local":
+                gs, gz = sticks[rank], planes[rank]
+            else:
+                gs, gz = max(1, ms), max(planes)
+            grid = G(nx, ny, nz, gs, PU, 1, max_local_z_length=gz, comm=TorchDistComm(),
                      exchange_type=getattr(sp.ExchangeType, exchange))
             t = grid.create_transform(PU, sp.TransformType.R2C if r2c else sp.TransformType.C2C,
                                       nx, ny, nz, planes[rank], parts[rank])
