@@ -246,6 +246,16 @@ def main():
     grid, t = grids[0], ts[0]
 
     plane = grid.data_plane if world > 1 else "none"
+    plane_info = grid.data_plane_info if world > 1 else {"kind": "none"}
+    # every GPU the job touched: the ranks' devices (PCI locations, gathered) and
+    # any relay GPUs the data plane uses besides them
+    prop = torch.cuda.get_device_properties(dev)
+    my_dev = f"{prop.pci_domain_id:04x}:{prop.pci_bus_id:02x}:{prop.pci_device_id:02x}"
+    rank_devs = [my_dev]
+    if dist is not None:
+        rank_devs = [None] * world
+        dist.all_gather_object(rank_devs, my_dev)
+    touched = list(dict.fromkeys(rank_devs + list(plane_info.get("devices", []))))
     if a.streams == "auto":
         a.streams = "one" if world == 1 else "per-transform"
     streams = []
@@ -334,15 +344,15 @@ def main():
         e = torch.tensor([float(sent)], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         exch["max_bytes_sent_per_rank"] = float(e.item())
+    # ranks that share a device (rehearsal on a small box) are not a multi-GPU
+    # measurement: record how many distinct devices the ranks ran on
+    n_devices = len(set(rank_devs))
     model = None
     if world > 1 and stages:
         chunks, blocks, peer_writes, relays = t.exchange_plan()
         model = _model(stages, exch["max_bytes_sent_per_rank"], world, chunks, blocks, relays)
         model["peer_writes"] = peer_writes
-        model["shared_device"] = min(world, ndev) < world
-    # ranks that share a device (rehearsal on a small box) are not a multi-GPU
-    # measurement: record how many distinct devices the job really used
-    n_devices = min(world, ndev)
+        model["shared_device"] = n_devices < world
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * T * a.steps / elapsed
     # the reference's FFT calls alone (rocFFT via
@@ -383,6 +393,9 @@ def main():
                 "exchange": a.exchange,
                 "data_plane": plane,
                 "distinct_devices": n_devices,
+                "devices_touched": touched,
+                "plane_info": plane_info,
+                "plane_self_test": plane_info.get("self_test"),
                 "shared_device": n_devices < world,
                 "sync": a.sync,
                 "streams": a.streams if T > 1 else "one",

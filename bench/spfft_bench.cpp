@@ -14,6 +14,9 @@
 //   --cutoff C      spherical cutoff |k/N| <= C instead of the slab sparsity
 //   --precision double|single
 //   --warmup W      untimed repeats before timing (default 1, as the reference)
+//   --stage-times   also time every GPU stage (a hipEvent per stage boundary;
+//                   the default timer tree holds host scopes only, like the
+//                   reference's rt_graph timer)
 //
 // With MPI (libspfft_amd_mpi present) the ranks of MPI_COMM_WORLD share the
 // grid: sticks and planes are split evenly, one GPU per rank (rank % devices).
@@ -47,6 +50,7 @@ struct Options {
   int dims[3] = {0, 0, 0};
   int repeats = -1;
   int warmup = 1;
+  bool stageTimes = false;
   int numTransforms = 1;
   double sparsity = 1.0;
   double cutoff = -1.0;
@@ -61,7 +65,7 @@ struct Options {
 [[noreturn]] void usage(const char* msg) {
   std::fprintf(stderr,
                "error: %s\nusage: spfft_bench -d X Y Z -r R -o FILE -e EXCH -p cpu|gpu|gpu-gpu "
-               "[-m M] [-s S] [-t c2c|r2c] [--cutoff C] [--precision double|single] [--warmup W]\n",
+               "[-m M] [-s S] [-t c2c|r2c] [--cutoff C] [--precision double|single] [--warmup W] [--stage-times]\n",
                msg);
   std::exit(2);
 }
@@ -109,6 +113,8 @@ Options parse(int argc, char** argv) {
     } else if (a == "--warmup") {
       need(i, 1);
       o.warmup = std::atoi(argv[++i]);
+    } else if (a == "--stage-times") {
+      o.stageTimes = true;
     } else if (a == "-h" || a == "--help") {
       usage("help");
     } else {
@@ -313,7 +319,7 @@ int main(int argc, char** argv) {
         throw std::runtime_error("no GPU visible for -p " + o.proc);
       (void)hipSetDevice(env.rank % ndev);
     }
-    (void)spfft_amd_timing_enable(1);
+    (void)spfft_amd_timing_enable(o.stageTimes ? 2 : 1);
     // even stick / plane split over ranks (reference: benchmark.cpp:166-198)
     const std::vector<Stick> sticks = make_sticks(o, r2c);
     const int S = static_cast<int>(sticks.size());

@@ -70,6 +70,12 @@ SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchan
  * grid). Collective on first call (creates the data plane). */
 SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name);
+/* The data plane's setup facts as a JSON object ("kind"; "self_test",
+ * "self_test_ms", "devices", "link_GBps_measured" where they apply). The string
+ * stays valid until the calling thread's next call of this function.
+ * Collective on first call. */
+SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane_info(SpfftGrid grid, const char** json);
+SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane_info(SpfftFloatGrid grid, const char** json);
 /* Device memory a grid allocated (exchange buffers, intermediate, space domain). */
 SPFFT_EXPORT SpfftError spfft_amd_grid_device_bytes(SpfftGrid grid, unsigned long long* bytes);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_device_bytes(SpfftFloatGrid grid,
@@ -128,7 +134,9 @@ SPFFT_EXPORT SpfftError spfft_amd_transform_backward_exchange(SpfftTransform t, 
 SPFFT_EXPORT SpfftError spfft_amd_transform_backward_xy(SpfftTransform t,
                                                         SpfftProcessingUnitType outputLocation);
 
-/* Host timer tree (enabled by SPFFT_TIMING=1 or spfft_amd_timing_enable(1)). */
+/* Timer tree (SPFFT_TIMING=1 or spfft_amd_timing_enable). enable: 0 off, 1 host
+ * scopes only (like the reference's timer), 2 host scopes and GPU stage times
+ * (a hipEvent per stage boundary, nodes gpu/<direction>/<stage>). */
 SPFFT_EXPORT SpfftError spfft_amd_timing_enable(int enable);
 SPFFT_EXPORT SpfftError spfft_amd_timing_reset(void);
 /* Writes a JSON report into buffer (truncated to size-1); *required = full length + 1. */

@@ -156,6 +156,16 @@ class _GridBase:
         return v.value.decode()
 
     @property
+    def data_plane_info(self) -> dict:
+        """The data plane's setup facts: "kind", and where they apply "self_test" /
+        "self_test_ms" (route self-test), "devices" (PCI bus ids of every GPU the plane
+        touches, relay GPUs included), "link_GBps_measured". Collective on first use."""
+        import json
+        v = ctypes.c_char_p()
+        _check(self._prec.amd_fn("grid_data_plane_info")(self._h, ctypes.byref(v)))
+        return json.loads(v.value.decode())
+
+    @property
     def device_bytes(self) -> int:
         """Device memory the grid allocated (exchange buffers, y/x intermediate, space)."""
         v = ctypes.c_ulonglong()

@@ -87,6 +87,8 @@ def _prototypes(lib):
     sig["spfft_amd_float_grid_exchange_type"] = [V, c_int_p]
     sig["spfft_amd_grid_data_plane"] = [V, ctypes.POINTER(ctypes.c_char_p)]
     sig["spfft_amd_float_grid_data_plane"] = [V, ctypes.POINTER(ctypes.c_char_p)]
+    sig["spfft_amd_grid_data_plane_info"] = [V, ctypes.POINTER(ctypes.c_char_p)]
+    sig["spfft_amd_float_grid_data_plane_info"] = [V, ctypes.POINTER(ctypes.c_char_p)]
     sig["spfft_amd_rccl_communicators"] = [c_int_p]
     sig["spfft_amd_library_streams"] = [c_int_p]
     sig["spfft_amd_grid_device_bytes"] = [V, ctypes.POINTER(ctypes.c_ulonglong)]

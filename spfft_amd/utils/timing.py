@@ -7,8 +7,10 @@ import json
 from ..ops._lib import lib
 
 
-def timing_enable(on: bool = True) -> None:
-    lib().spfft_amd_timing_enable(1 if on else 0)
+def timing_enable(on: bool = True, gpu_stages: bool = True) -> None:
+    """Host timer scopes, plus (gpu_stages) hipEvent intervals of every GPU stage
+    under gpu/<direction>/<stage>."""
+    lib().spfft_amd_timing_enable((2 if gpu_stages else 1) if on else 0)
 
 
 def timing_reset() -> None:

@@ -147,6 +147,16 @@ const char* data_plane_of(Impl& impl) {
   if (!(impl.processing_unit() & SPFFT_PU_GPU) || impl.local()) return "none";
   return impl.device_comm().kind();
 }
+// (a per-thread copy: valid until the thread's next call)
+template <class Impl>
+const char* data_plane_info_of(Impl& impl) {
+  static thread_local std::string buf;
+  if (!(impl.processing_unit() & SPFFT_PU_GPU) || impl.local())
+    buf = "{\"kind\": \"none\"}";
+  else
+    buf = impl.device_comm().info_json();
+  return buf.c_str();
+}
 }  // namespace
 
 namespace {
@@ -416,6 +426,14 @@ SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** nam
   if (!name) return SPFFT_INVALID_PARAMETER_ERROR;
   return with_handle<GridFloat>(grid, [&](GridFloat& g) { *name = data_plane_of(*g.impl()); });
 }
+SpfftError spfft_amd_grid_data_plane_info(SpfftGrid grid, const char** json) {
+  if (!json) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<Grid>(grid, [&](Grid& g) { *json = data_plane_info_of(*g.impl()); });
+}
+SpfftError spfft_amd_float_grid_data_plane_info(SpfftFloatGrid grid, const char** json) {
+  if (!json) return SPFFT_INVALID_PARAMETER_ERROR;
+  return with_handle<GridFloat>(grid, [&](GridFloat& g) { *json = data_plane_info_of(*g.impl()); });
+}
 
 SpfftError spfft_amd_grid_device_bytes(SpfftGrid grid, unsigned long long* bytes) {
   if (!bytes) return SPFFT_INVALID_PARAMETER_ERROR;
@@ -518,7 +536,7 @@ SpfftError spfft_amd_transform_backward_xy(SpfftTransform t, SpfftProcessingUnit
 }
 
 SpfftError spfft_amd_timing_enable(int enable) {
-  timing::set_enabled(enable != 0);
+  timing::set_level(enable);
   return SPFFT_SUCCESS;
 }
 SpfftError spfft_amd_timing_reset(void) {

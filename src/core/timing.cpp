@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <string>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -28,10 +29,13 @@ struct Node {
 struct Registry {
   std::mutex mutex;
   Node root;
-  std::atomic<bool> on{false};
+  std::atomic<int> level{0};
   Registry() {
+    // SPFFT_TIMING=1 (or any value but 0 / host): host scopes and GPU stage
+    // events; SPFFT_TIMING=host: host scopes only
     const char* env = std::getenv("SPFFT_TIMING");
-    on = env && env[0] != '\0' && env[0] != '0';
+    const std::string v = env ? env : "";
+    level = v.empty() || v == "0" ? 0 : (v == "host" ? 1 : 2);
     root.name = "root";
   }
 };
@@ -127,8 +131,9 @@ void text_node(const Node& n, int depth, double parentTotal, double rootTotal,
 
 }  // namespace
 
-bool enabled() { return registry().on.load(std::memory_order_relaxed); }
-void set_enabled(bool on) { registry().on = on; }
+bool enabled() { return registry().level.load(std::memory_order_relaxed) > 0; }
+bool gpu_stages() { return registry().level.load(std::memory_order_relaxed) > 1; }
+void set_level(int level) { registry().level = level < 0 ? 0 : (level > 2 ? 2 : level); }
 
 void reset() {
   auto& r = registry();

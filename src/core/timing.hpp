@@ -13,8 +13,12 @@
 namespace spfft {
 namespace timing {
 
+// Level 0 off, 1 host scopes (the reference's rt_graph timer), 2 host scopes
+// plus GPU stage intervals (hipEvents at every stage boundary, one record per
+// stage: extra host API calls on every transform).
 bool enabled();
-void set_enabled(bool on);
+bool gpu_stages();
+void set_level(int level);
 void reset();
 std::string report_json();
 std::string report_text();

@@ -257,6 +257,47 @@ std::map<std::string, std::weak_ptr<NcclChannel>>& channel_registry() {
 }
 std::atomic<int> gChannelsCreated{0};
 
+// PCI location of a device ordinal of this process
+struct PciId {
+  int domain, bus, device;
+  bool operator==(const PciId& o) const { return domain == o.domain && bus == o.bus && device == o.device; }
+};
+PciId pci_of(int ordinal) {
+  PciId id{-1, -1, -1};
+  (void)hipDeviceGetAttribute(&id.domain, hipDeviceAttributePciDomainID, ordinal);
+  (void)hipDeviceGetAttribute(&id.bus, hipDeviceAttributePciBusId, ordinal);
+  (void)hipDeviceGetAttribute(&id.device, hipDeviceAttributePciDeviceId, ordinal);
+  (void)hipGetLastError();
+  return id;
+}
+
+// "dddd:bb:dd" of a PCI location
+std::string pci_string(const PciId& id) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "%04x:%02x:%02x", id.domain & 0xffff, id.bus & 0xff, id.device & 0xff);
+  return b;
+}
+
+// JSON list of the distinct entries of `ids`, in first-seen order
+std::string json_distinct(const std::vector<std::string>& ids) {
+  std::vector<std::string> seen;
+  for (const std::string& i : ids)
+    if (std::find(seen.begin(), seen.end(), i) == seen.end()) seen.push_back(i);
+  std::string o = "[";
+  for (std::size_t k = 0; k < seen.size(); ++k) o += (k ? ", \"" : "\"") + seen[k] + "\"";
+  return o + "]";
+}
+
+// Every rank's device, as PCI location strings (collective)
+std::vector<std::string> group_devices(Communicator& comm, int device) {
+  PciId mine = pci_of(device);
+  std::vector<PciId> all(comm.size());
+  comm.allgather(&mine, all.data(), sizeof(PciId));
+  std::vector<std::string> out;
+  for (const PciId& q : all) out.push_back(pci_string(q));
+  return out;
+}
+
 // SPFFT_FAULT_EXCHANGE_ABORT=N (fault injection, failure-detection tests): the
 // N-th exchange of a data plane aborts its RCCL communicator first, so that
 // exchange and every later one fail with MPIError
@@ -577,6 +618,7 @@ public:
                 "hipDeviceGetAttribute");
       timeoutTicks_ = static_cast<long long>(peer_timeout_seconds() * 1e3 * std::max(rateKHz, 1));
       comm_->barrier();  // every flag array is zeroed before the first barrier round
+      devices_ = group_devices(*comm_, device);
       self_test();
       return;
     } else {
@@ -672,6 +714,15 @@ public:
     __atomic_fetch_or(failHost_, kAborted, __ATOMIC_ACQ_REL);
   }
   const char* kind() const override { return ipc_ ? "ipc" : "peer"; }
+  std::string info_json() const override {
+    char b[512];
+    const char* where = mode_ == PeerBarrier::kStream ? "stream" : mode_ == PeerBarrier::kChannel ? "channel" : "host";
+    std::snprintf(b, sizeof(b),
+                  "{\"kind\": \"%s\", \"ranks\": %d, \"barrier\": \"%s\", \"xcd_mask\": %u, "
+                  "\"self_test\": \"%s\", \"self_test_ms\": %.3f, \"devices\": %s}",
+                  kind(), P_, where, xcdMask_, selfTest_.c_str(), selfTestMs_, json_distinct(devices_).c_str());
+    return b;
+  }
   std::string describe() const override {
     if (!ipc_) return kind();
     const IpcArenaStats s = ipc_arena_stats();
@@ -897,6 +948,7 @@ private:
   bool readPending_[2] = {false, false};
   std::string selfTest_ = "not run";
   double selfTestMs_ = 0;
+  std::vector<std::string> devices_;  // every rank's GPU (PCI location)
 };
 
 // ------------------------------------------------------------ relay routing
@@ -1038,8 +1090,12 @@ public:
     // the per-exchange host collectives (one allgather, two barriers) through
     // shared memory when every rank maps the segment, else through comm
     shm_ = ShmGroup::create(*comm_, sizeof(Transfer) * static_cast<std::size_t>(2 * P_ + 1), comm_timeout_seconds());
+    devices_ = group_devices(*comm_, device);
+    for (int c : relayDev_) devices_.push_back(pci_string(pci_of(c)));
     comm_->barrier();
+    const auto t0 = std::chrono::steady_clock::now();
     self_test();
+    selfTestMs_ = 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
   // Collective. One exchange of a known pattern through every route (direct
@@ -1202,6 +1258,14 @@ public:
     return d + (shm_ ? "; host sync: shared memory)" : "; host sync: communicator)");
   }
   int relay_count() const override { return K_; }
+  std::string info_json() const override {
+    char b[512];
+    std::snprintf(b, sizeof(b),
+                  "{\"kind\": \"relay\", \"ranks\": %d, \"relay_gpus\": %d, \"self_test\": \"ok\", "
+                  "\"self_test_ms\": %.3f, \"devices\": %s}",
+                  P_, K_, selfTestMs_, json_distinct(devices_).c_str());
+    return b;
+  }
 
 private:
   static constexpr int kMaxRelays = 8;
@@ -1251,6 +1315,8 @@ private:
   long long minBytes_ = 0;
   std::size_t relayCap_ = 0;
   std::vector<long long> capOf_;     // every rank's relay capacity (per relay buffer)
+  std::vector<std::string> devices_;  // ranks' GPUs and relay GPUs (PCI locations)
+  double selfTestMs_ = 0;
   unsigned long long minSide_ = 0;   // smallest exchange side of the group
   std::unique_ptr<IpcLease> sides_[2];
   std::vector<std::unique_ptr<IpcLease>> relay_;
@@ -1295,20 +1361,6 @@ int env_relay() {
   const char* e = std::getenv("SPFFT_RELAY");
   const std::string v = e ? e : "";
   return v == "0" || v == "off" ? 1 : (v == "force" ? 2 : 0);
-}
-
-// PCI location of a device ordinal of this process
-struct PciId {
-  int domain, bus, device;
-  bool operator==(const PciId& o) const { return domain == o.domain && bus == o.bus && device == o.device; }
-};
-PciId pci_of(int ordinal) {
-  PciId id{-1, -1, -1};
-  (void)hipDeviceGetAttribute(&id.domain, hipDeviceAttributePciDomainID, ordinal);
-  (void)hipDeviceGetAttribute(&id.bus, hipDeviceAttributePciBusId, ordinal);
-  (void)hipDeviceGetAttribute(&id.device, hipDeviceAttributePciDeviceId, ordinal);
-  (void)hipGetLastError();
-  return id;
 }
 
 // Collective. The GPUs of this node that no rank of the group runs on and

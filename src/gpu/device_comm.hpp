@@ -141,6 +141,11 @@ public:
   virtual const char* kind() const = 0;
   // One line for SPFFT_LOG (e.g. which RCCL communicator a grid uses).
   virtual std::string describe() const { return kind(); }
+  // The plane's setup facts as one JSON object: "kind", and where they apply
+  // "self_test" / "self_test_ms" (route self-test at setup), "devices" (PCI
+  // bus ids of every GPU the plane touches: the ranks' and any relay GPUs),
+  // "link_GBps_measured" (copy probe at setup). Stable for the plane's life.
+  virtual std::string info_json() const { return std::string("{\"kind\": \"") + kind() + "\"}"; }
   // RCCL communicators this process has created (shared channels count once).
   static int rccl_channels_created();
 };

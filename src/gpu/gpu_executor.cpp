@@ -443,7 +443,7 @@ void GpuExecutor<T>::run_steps(const std::vector<ExchangeStep>& steps, bool back
   // SPFFT_TIMING: the span from the first step's start to the last step's
   // completion on the data plane's stream (gpu/<direction>/exchange-span)
   GpuEvent *b = nullptr, *e = nullptr;
-  if (timing::enabled() && !capturing_ && !steps.empty()) {
+  if (timing::gpu_stages() && !capturing_ && !steps.empty()) {
     spans_.push_back(ExchangeSpan{backward ? "backward" : "forward", timing_event(), timing_event()});
     b = spans_.back().begin.get();
     e = spans_.back().end.get();
@@ -585,7 +585,7 @@ void GpuExecutor<T>::wait_stream() {
 // ---------------------------------------------------------- stage timing
 template <typename T>
 void GpuExecutor<T>::stage_mark(const char* dir, const char* stage) {
-  if (!timing::enabled() || capturing_) return;
+  if (!timing::gpu_stages() || capturing_) return;
   if (!stage) {
     // a direction starts: collect what has completed, bound the backlog
     harvest_stage_times(traces_.size() >= 64);

@@ -250,6 +250,28 @@ def test_ipc_grid_churn_uneven_teardown(gpu):
 
 
 @pytest.mark.gpu
+def test_ipc_peer_self_test(gpu):
+    """The peer-write plane checks its route at setup (every receiver's L2 warmed
+    with the old contents, stage-kernel-style remote stores, one barrier round, every
+    word checked) and records the outcome in the plane info."""
+    code, out = _launch_tool(3, "rccl_probe.py", "UNBUFFERED", "--iters=2", timeout=180)
+    assert code == 0, out[-4000:]
+    assert out.count("[ipc] self-test: ok") == 3, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_ipc_peer_self_test_failure_detected(gpu):
+    """A wrong word in the self-test (fault injection: the last rank corrupts its
+    message to rank 0) fails the plane on every rank. Ranks that share one GPU have no
+    other plane (RCCL refuses them), so grid setup raises MPIError everywhere; ranks
+    on distinct GPUs fall back to RCCL (DeviceComm::create)."""
+    code, out = _launch_tool(2, "rccl_probe.py", "UNBUFFERED", env_extra={"SPFFT_FAULT_PEER_SELFTEST": "1"},
+                             timeout=180)
+    assert code != 0, out[-4000:]
+    assert out.count("route self-test failed") >= 2, out[-4000:]
+
+
+@pytest.mark.gpu
 def test_ipc_stale_mapping_detected(gpu, monkeypatch):
     """A mapping whose header does not carry the owner's announced nonce (fault
     injection: the last rank announces a wrong one) is reported as MPIError on
@@ -341,3 +363,18 @@ def test_relay_self_test_failure_falls_back(gpu, monkeypatch):
     code, out = _launch_tool(2, "rccl_probe.py", "COMPACT_BUFFERED", "--iters=2")
     assert code == 0, out[-4000:]
     assert out.count("[ipc]") == 2 and "self-test exchange delivered wrong data" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plane", ["ipc", "relay"])
+def test_fuzz_dist_local_maxima(gpu, plane):
+    """Every rank passes its own stick and plane counts as the grid maxima (zero on
+    empty ranks), so the exchange sides differ per rank (the reference allows this,
+    grid_internal.cpp:190): the relay split must use each sender's own capacity and
+    the self-tests a message size every rank can hold."""
+    env = {"SPFFT_RELAY": "force", "SPFFT_RELAY_MIN_BYTES": "0", "SPFFT_RELAY_VIRTUAL": "2"} \
+        if plane == "relay" else {}
+    code, out = _launch_tool(3, "fuzz_dist.py", "--cases", "24", "--seed", "21", "--maxima", "local",
+                             env_extra=env)
+    assert code == 0, out[-4000:]
+    assert "24/24 passed" in out and f"plane={plane}" in out, out[-4000:]

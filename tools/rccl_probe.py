@@ -68,6 +68,8 @@ def main():
     tol = 1e-5 if "FLOAT" in exch_name else 1e-11
     ok = e1 < tol and e2 < tol
     kind = "" if host else f" [{s.grid.data_plane}]"
+    if not host and s.grid.data_plane in ("ipc", "relay"):
+        kind += f" self-test: {s.grid.data_plane_info.get('self_test')}"
     print(f"rank {rank}/{P} {exch_name}{kind} x{iters}: backward err {e1:.2e} forward err {e2:.2e} "
           f"{'OK' if ok else 'FAIL'}", flush=True)
     del s
