@@ -47,14 +47,6 @@ SPFFT_EXPORT SpfftError spfft_amd_comm_create_local_group(int size, SpfftAmdComm
 SPFFT_EXPORT SpfftError spfft_amd_comm_destroy(SpfftAmdComm comm);
 SPFFT_EXPORT SpfftError spfft_amd_comm_rank(SpfftAmdComm comm, int* rank);
 SPFFT_EXPORT SpfftError spfft_amd_comm_size(SpfftAmdComm comm, int* size);
-/* Collective. Node-local shared-memory collectives (the relay data plane's host
-   synchronisation) over `comm`: `iters` rounds of a checked allgather plus a barrier
-   through one shared segment, then the same through the communicator itself.
-   *shmUs / *commUs: microseconds per round (shmUs < 0 if the ranks could not share a
-   segment). SPFFT_MPI_ERROR if a round delivered wrong data. */
-SPFFT_EXPORT SpfftError spfft_amd_comm_shm_check(SpfftAmdComm comm, int iters, double* shmUs,
-                                                 double* commUs);
-
 SPFFT_EXPORT SpfftError spfft_amd_grid_create_distributed(
     SpfftGrid* grid, int maxDimX, int maxDimY, int maxDimZ, int maxNumLocalZColumns,
     int maxLocalZLength, SpfftProcessingUnitType processingUnit, int maxNumThreads,

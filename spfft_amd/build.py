@@ -60,7 +60,9 @@ def _install(src, dst):
 
 def _check_targets():
     """Every kernel object must carry a gfx950 code object (and nothing else)."""
-    objs = glob.glob(os.path.join(BUILD_DIR, "CMakeFiles", "spfft_amd.dir", "src", "kernels", "*.o"))
+    objs = glob.glob(os.path.join(BUILD_DIR, "CMakeFiles", "spfft_amd_kernels.dir", "src", "kernels", "*.o"))
+    if not objs:
+        raise RuntimeError("no kernel objects found under CMakeFiles/spfft_amd_kernels.dir")
     llvm = os.path.join(ROCM, "llvm", "bin")
     for o in objs:
         tmp = o + ".fatbin"

@@ -14,6 +14,9 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 NATIVE_DIR = os.path.join(os.path.dirname(_HERE), "_native")
 LIB_NAME = "libspfft_amd.so"
+# the testing library: the same kernels and host code plus fault injection and
+# test probes (CMake SPFFT_TESTING_LIBRARY); loaded when SPFFT_AMD_LIBRARY names it
+TESTING_LIB_PATH = os.path.join(NATIVE_DIR, "libspfft_amd_testing.so")
 
 _lock = threading.Lock()
 _lib = None
@@ -80,7 +83,6 @@ def _prototypes(lib):
     sig["spfft_amd_comm_destroy"] = [V]
     sig["spfft_amd_comm_rank"] = [V, c_int_p]
     sig["spfft_amd_comm_size"] = [V, c_int_p]
-    sig["spfft_amd_comm_shm_check"] = [V, I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     sig["spfft_amd_grid_create_distributed"] = [c_void_pp, I, I, I, I, I, I, I, V, I]
     sig["spfft_amd_float_grid_create_distributed"] = [c_void_pp, I, I, I, I, I, I, I, V, I]
     sig["spfft_amd_grid_exchange_type"] = [V, c_int_p]
@@ -114,6 +116,12 @@ def _prototypes(lib):
     sig["spfft_amd_timing_reset"] = []
     sig["spfft_amd_timing_json"] = [ctypes.c_char_p, ctypes.c_size_t, c_size_t_p]
     sig["spfft_amd_timing_print"] = [ctypes.c_char_p, ctypes.c_size_t, c_size_t_p]
+    # test probes: present in the testing library only
+    test_sig = {"spfft_amd_test_comm_shm_check": [V, I, ctypes.POINTER(ctypes.c_double),
+                                                  ctypes.POINTER(ctypes.c_double)]}
+    for name, args in test_sig.items():
+        if hasattr(lib, name):
+            sig[name] = args
     for name, args in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -124,6 +132,11 @@ def _prototypes(lib):
     lib.spfft_amd_device_count.restype = ctypes.c_int
     lib.spfft_amd_build_info.argtypes = []
     lib.spfft_amd_build_info.restype = ctypes.c_char_p
+
+
+def is_testing_library() -> bool:
+    """True if the loaded library is the testing build (fault injection, probes)."""
+    return hasattr(lib(), "spfft_amd_test_fault_injection")
 
 
 def lib():

@@ -39,8 +39,12 @@ class Communicator:
         synchronisation) against this communicator's own: microseconds per checked
         allgather + barrier round, ``(shm_us, comm_us)``; ``shm_us`` is None when the
         ranks cannot share a segment."""
+        L = lib()
+        if not hasattr(L, "spfft_amd_test_comm_shm_check"):
+            raise RuntimeError("shm_check is a probe of the testing library: set SPFFT_AMD_LIBRARY to "
+                               "spfft_amd/_native/libspfft_amd_testing.so")
         shm, com = ctypes.c_double(), ctypes.c_double()
-        _check(lib().spfft_amd_comm_shm_check(self.handle, int(iters), ctypes.byref(shm), ctypes.byref(com)))
+        _check(L.spfft_amd_test_comm_shm_check(self.handle, int(iters), ctypes.byref(shm), ctypes.byref(com)))
         return (shm.value if shm.value >= 0 else None), com.value
 
     def __del__(self):

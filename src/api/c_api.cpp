@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "api/c_guard.hpp"
 #include "api/transform_impl.hpp"
 #include "comm/callback_comm.hpp"
 #include "comm/shm_group.hpp"
@@ -36,29 +37,12 @@ void multi_backward_handles(int n, TransformFloat** ts, float** in, SpfftProcess
 
 using namespace spfft;
 
-namespace {
-
-thread_local std::string tlsLastError;
-
-template <class F>
-SpfftError guarded(F&& f) {
-  error_detail().clear();
-  try {
-    f();
-    tlsLastError.clear();
-    return SPFFT_SUCCESS;
-  } catch (const GenericError& e) {
-    tlsLastError = e.what();
-    if (!error_detail().empty()) tlsLastError += " [" + error_detail() + "]";
-    return e.error_code();
-  } catch (const std::exception& e) {
-    tlsLastError = e.what();
-    return SPFFT_UNKNOWN_ERROR;
-  } catch (...) {
-    tlsLastError = "unknown error";
-    return SPFFT_UNKNOWN_ERROR;
-  }
+std::string& spfft::c_last_error() {
+  static thread_local std::string msg;
+  return msg;
 }
+
+namespace {
 
 template <class H>
 H* handle(void* h) {
@@ -71,13 +55,12 @@ struct InvalidHandle {};
 template <class H, class F>
 SpfftError with_handle(void* h, F&& f) {
   if (!h) {
-    tlsLastError = "invalid handle";
+    c_last_error() = "invalid handle";
     return SPFFT_INVALID_HANDLE_ERROR;
   }
   return guarded([&] { f(*static_cast<H*>(h)); });
 }
 
-using CommHandle = std::shared_ptr<Communicator>;
 
 // Minimal DLPack (v0.8 ABI) structures for zero-copy export of the space domain.
 struct DLDeviceX {
@@ -349,42 +332,6 @@ SpfftError spfft_amd_comm_size(SpfftAmdComm comm, int* size) {
   return with_handle<CommHandle>(comm, [&](CommHandle& c) { *size = c->size(); });
 }
 
-SpfftError spfft_amd_comm_shm_check(SpfftAmdComm comm, int iters, double* shmUs, double* commUs) {
-  if (!shmUs || !commUs || iters < 1) return SPFFT_INVALID_PARAMETER_ERROR;
-  return with_handle<CommHandle>(comm, [&](CommHandle& c) {
-    Communicator& cm = *c;
-    const int P = cm.size(), me = cm.rank();
-    std::vector<long long> mine(4), all(static_cast<std::size_t>(4) * P);
-    auto round = [&](int it, auto&& gather, auto&& barrier) {
-      for (int k = 0; k < 4; ++k) mine[k] = (static_cast<long long>(it) << 20) + me * 4 + k;
-      gather(mine.data(), all.data(), mine.size() * sizeof(long long));
-      for (int q = 0; q < P; ++q)
-        for (int k = 0; k < 4; ++k)
-          if (all[static_cast<std::size_t>(q) * 4 + k] != (static_cast<long long>(it) << 20) + q * 4 + k) {
-            set_error_detail("shared-memory allgather delivered wrong data");
-            throw MPIError();
-          }
-      barrier();
-    };
-    auto timed = [&](auto&& gather, auto&& barrier) {
-      round(-1, gather, barrier);
-      const auto t0 = std::chrono::steady_clock::now();
-      for (int it = 0; it < iters; ++it) round(it, gather, barrier);
-      return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
-    };
-    auto shm = ShmGroup::create(cm, mine.size() * sizeof(long long), 60.0);
-    // fault injection (tests): the last rank leaves without a word; the others'
-    // shared-memory waits must end with MPIError, not spin
-    const char* fi = std::getenv("SPFFT_FAULT_SHM_EXIT");
-    if (shm && fi && *fi == '1' && me == P - 1 && P > 1) std::_Exit(0);
-    *shmUs = shm ? timed([&](const void* s, void* r, std::size_t n) { shm->allgather(s, r, n); },
-                         [&] { shm->barrier(); })
-                 : -1.0;
-    *commUs = timed([&](const void* s, void* r, std::size_t n) { cm.allgather(s, r, n); },
-                    [&] { cm.barrier(); });
-  });
-}
-
 SpfftError spfft_amd_grid_create_distributed(SpfftGrid* grid, int maxDimX, int maxDimY,
                                              int maxDimZ, int maxNumLocalZColumns,
                                              int maxLocalZLength,
@@ -561,7 +508,7 @@ SpfftError spfft_amd_timing_print(char* buffer, size_t size, size_t* required) {
   return copy_report(timing::report_text(), buffer, size, required);
 }
 
-const char* spfft_amd_last_error_message(void) { return tlsLastError.c_str(); }
+const char* spfft_amd_last_error_message(void) { return c_last_error().c_str(); }
 
 int spfft_amd_device_count(void) {
   int n = 0;

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "core/common.hpp"
+#include "core/fault.hpp"
 #include "core/timing.hpp"
 #include "gpu/gpu_runtime.hpp"
 #include "gpu/ipc_arena.hpp"
@@ -137,7 +138,7 @@ struct NcclChannel {
     // fault injection: 1 = every rank fails, 2 = only the last rank fails (the
     // others then wait for it until the init deadline and abort)
     if (injectFault == 1 || (injectFault == 2 && rank == size - 1)) {
-      detail = "RCCL: initialisation failure injected (SPFFT_FAULT_RCCL_INIT)";
+      detail = "RCCL: initialisation failure injected (fault injection RCCL_INIT)";
       return;
     }
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -298,13 +299,10 @@ std::vector<std::string> group_devices(Communicator& comm, int device) {
   return out;
 }
 
-// SPFFT_FAULT_EXCHANGE_ABORT=N (fault injection, failure-detection tests): the
+// Fault injection EXCHANGE_ABORT = N (testing library, core/fault.hpp): the
 // N-th exchange of a data plane aborts its RCCL communicator first, so that
 // exchange and every later one fail with MPIError
-int fault_abort_at() {
-  const char* e = std::getenv("SPFFT_FAULT_EXCHANGE_ABORT");
-  return e && *e ? std::atoi(e) : 0;
-}
+int fault_abort_at() { return SPFFT_FAULT(EXCHANGE_ABORT); }
 
 class RcclDeviceComm : public DeviceComm {
 public:
@@ -580,12 +578,9 @@ unsigned long long fresh_test_nonce() {
   return ((static_cast<unsigned long long>(rd()) << 32) ^ rd() ^ t ^ static_cast<unsigned long long>(getpid())) | 1ull;
 }
 
-// Fault injection (tests): the last rank corrupts one word of its message to
-// rank 0 in the peer plane's self-test.
-bool fault_flag_peer_selftest() {
-  const char* e = std::getenv("SPFFT_FAULT_PEER_SELFTEST");
-  return e && *e == '1';
-}
+// Fault injection PEER_SELFTEST (testing library): the last rank corrupts one
+// word of its message to rank 0 in the peer plane's self-test.
+bool fault_flag_peer_selftest() { return SPFFT_FAULT(PEER_SELFTEST) == 1; }
 
 class PeerDeviceComm : public DeviceComm {
 public:
@@ -759,10 +754,9 @@ private:
       for (int i = 0; i < 2; ++i)
         if (sides_[i]) mine.e[i] = sides_[i]->describe();
       mine.e[2] = flags_->describe();
-      // fault injection (SPFFT_FAULT_IPC_NONCE=1): the last rank announces a
-      // nonce its flag array does not carry, as a stale mapping would show
-      const char* fi = std::getenv("SPFFT_FAULT_IPC_NONCE");
-      if (fi && *fi == '1' && me_ == P_ - 1) mine.e[2].header.nonce ^= 1;
+      // fault injection IPC_NONCE (testing library): the last rank announces
+      // a nonce its flag array does not carry, as a stale mapping would show
+      if (SPFFT_FAULT(IPC_NONCE) == 1 && me_ == P_ - 1) mine.e[2].header.nonce ^= 1;
     } catch (const std::exception& ex) {
       res.ok = 0;
       std::snprintf(res.why, sizeof(res.why), "IPC arena: %s", ex.what());
@@ -1119,8 +1113,8 @@ public:
       };
       for (int q = 0; q < P_; ++q)
         for (int i = 0; i < words; ++i) pattern[static_cast<std::size_t>(q) * words + i] = word(me_, q, i);
-      const char* fi = std::getenv("SPFFT_FAULT_RELAY_SELFTEST");
-      if (fi && *fi == '1' && me_ == P_ - 1 && P_ > 1) pattern[static_cast<std::size_t>((me_ + 1) % P_) * words] ^= 1;
+      // fault injection RELAY_SELFTEST (testing library)
+      if (SPFFT_FAULT(RELAY_SELFTEST) == 1 && me_ == P_ - 1 && P_ > 1) pattern[static_cast<std::size_t>((me_ + 1) % P_) * words] ^= 1;
       void* send = sides_[0]->data();
       void* recv = sides_[1]->data();
       gpu_check(hipMemcpy(send, pattern.data(), pattern.size() * 8, hipMemcpyHostToDevice), "hipMemcpy");
@@ -1335,7 +1329,7 @@ struct NodeInfo {
   int domain, bus, device, ordinal;
   unsigned long long channelDomain;  // Communicator::channel_domain
   int prefer;  // SPFFT_GPU_EXCHANGE: 0 auto, 1 rccl, 2 peer (ipc)
-  int fault;   // SPFFT_FAULT_RCCL_INIT (rank 0's value is used everywhere)
+  int fault;   // fault injection RCCL_INIT (rank 0's value is used everywhere)
   int relay;   // SPFFT_RELAY: 0 auto, 1 off, 2 force (virtual relays)
   int relayVirtual;  // SPFFT_RELAY_VIRTUAL
   unsigned long long stickBytes;  // this rank's stick side (per-peer message estimate)
@@ -1419,10 +1413,7 @@ int env_choice(const char* name) {
   return v == "rccl" ? 1 : (v == "ipc" || v == "peer" ? 2 : 0);
 }
 
-int env_fault() {
-  const char* e = std::getenv("SPFFT_FAULT_RCCL_INIT");
-  return e && *e ? std::atoi(e) : 0;
-}
+int env_fault() { return SPFFT_FAULT(RCCL_INIT); }
 
 bool share_channels() {
   const char* e = std::getenv("SPFFT_RCCL_SHARE");

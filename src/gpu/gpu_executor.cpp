@@ -16,18 +16,6 @@
 
 namespace spfft {
 
-namespace {
-// A/B switch (profiles/r6/shared_gpu): 1 = every wave of a stage kernel that
-// stores into peers' memory ends with a system-scope release (the round-5
-// form); 0 (default) = the barrier round's per-XCD write-back publishes them.
-int stage_release_fence() {
-  static const int v = [] {
-    const char* e = std::getenv("SPFFT_STAGE_RELEASE");
-    return e && *e == '1' ? 1 : 0;
-  }();
-  return v;
-}
-}  // namespace
 
 
 namespace {
@@ -59,9 +47,8 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   floatExchange_ = distributed && is_exchange_float(grid_->exchange_type());
   const int stickElemBytes = floatExchange_ ? sizeof(cx<float>) : sizeof(cx<T>);
   layout_ = make_exchange_layout(p, distributed && is_exchange_buffered(grid_->exchange_type()),
-                                 env_int("SPFFT_PAD_STICK", aligned_row_pad(p.dimZ, stickElemBytes), 0,
-                                         kMaxPad));
-  interStride_ = p.dimY + env_int("SPFFT_PAD_INTER", aligned_row_pad(p.dimY, sizeof(cx<T>)), 0, kMaxPad);
+                                 aligned_row_pad(p.dimZ, stickElemBytes));
+  interStride_ = p.dimY + aligned_row_pad(p.dimY, sizeof(cx<T>));
   poison_ = env_int("SPFFT_POISON", 0, 0, 1) != 0;
   // opt-in: on ROCm 7.2 a replayed graph was measured slower than direct
   // launches in stream-ordered use (profiles/README.md, session 6)
@@ -99,7 +86,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
   upload(colY_, p.colY);
   std::vector<long long> cb(layout_.colEntryBase.begin(), layout_.colEntryBase.end());
   upload(colBase_, cb);
-  colDescs_ = env_int("SPFFT_COL_DESC", 1, 0, 1) != 0;
+  colDescs_ = true;
   build_col_desc(colDesc_, cb, layout_.slabStride);
   upload(colX_, p.colX);
   if (longX_) upload(xToCol_, p.xToCol);
@@ -128,7 +115,7 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     // collective data-plane setup happens at plan time
     peerWrites_ = grid_->device_comm().peer_writes();
     if (peerWrites_) build_peer_tables();
-    localDirect_ = !peerWrites_ && env_int("SPFFT_LOCAL_DIRECT", 1, 0, 1) != 0;
+    localDirect_ = !peerWrites_;
     if (localDirect_) {
       // this rank's own block never moves: the z stage writes it straight into
       // its place on the slab side (where the y stage and, forward, the z stage
@@ -918,7 +905,8 @@ void GpuExecutor<T>::backward_z(const T* input) {
     // the z stage stores straight into the peers' slab sides
     grid_->device_comm().prepare_write(GridImpl<T>::kSlabSide, stream_);
     a.zTab = zTabRemote_->data<long long>();
-    a.remote = stage_release_fence();
+    // (no fence in the kernel: the barrier round after it writes back every
+    // XCD's L2, peer_sync.hip)
   }
   // pipelined plans: one launch per stick block, whose messages leave as soon
   // as it is done (zEv_, run_steps)
@@ -1165,7 +1153,6 @@ void GpuExecutor<T>::forward_xy(SpfftProcessingUnitType inputLocation) {
       } else if (peerWrites_) {
         ya.colBase = colBaseRemote_ ? colBaseRemote_->data<long long>() : nullptr;
         set_col_desc(ya, colDescRemote_);
-        ya.remote = stage_release_fence();
       }
       cx<T>* out = inter_for(inter, z0);
       x_forward_launch(xa, space, out);

@@ -41,7 +41,7 @@ std::uint64_t gSerial = 0;
 std::size_t pool_cap() {
   static const std::size_t cap = [] {
     const char* e = std::getenv("SPFFT_IPC_POOL_BYTES");
-    return e && *e ? static_cast<std::size_t>(std::atof(e)) : (std::size_t(4) << 30);
+    return e && *e ? static_cast<std::size_t>(std::atof(e)) : (std::size_t(2) << 30);
   }();
   return cap;
 }
@@ -57,20 +57,8 @@ std::uint64_t fresh_nonce(std::uint64_t serial) {
   return n;
 }
 
-// SPFFT_IPC_ARENA=0 (documented A/B switch, profiles/r5/ipc): exact-size
-// blocks, freed when their lease ends: the round-4 allocation lifetime, with
-// the header check still in place, to show what the arena prevents.
-bool arena_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("SPFFT_IPC_ARENA");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 std::size_t round_block(std::size_t payload) {
   const std::size_t need = payload + kIpcHeaderBytes;
-  if (!arena_on()) return need;
   return ((need + kIpcBlockGranule - 1) / kIpcBlockGranule) * kIpcBlockGranule;
 }
 
@@ -160,7 +148,7 @@ std::unique_ptr<IpcLease> ipc_acquire(int device, std::size_t payloadBytes, bool
 IpcLease::~IpcLease() {
   if (!block_) return;
   std::lock_guard<std::mutex> lock(gArenaMutex);
-  if (discard_ || !arena_on()) {
+  if (discard_) {
     free_block(block_);
     return;
   }

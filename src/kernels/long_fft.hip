@@ -17,22 +17,19 @@ namespace spfft {
 namespace dev {
 
 // ------------------------------------------------------------ glue helpers
-// f(i) for i in [0, n), grid-stride; fence: release this thread's stores
-// system-wide at the end (peer-write exchange)
+// f(i) for i in [0, n), grid-stride
 template <class F>
-__global__ void __launch_bounds__(256) for_each_kernel(long long n, int fence, F f) {
+__global__ void __launch_bounds__(256) for_each_kernel(long long n, F f) {
   const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n; i += stride)
     f(i);
-  release_remote(fence);
 }
 
 template <class F>
-void for_each(long long n, hipStream_t s, F f, int fence = 0) {
+void for_each(long long n, hipStream_t s, F f) {
   if (n <= 0) return;
   const long long blocks = std::min<long long>((n + 255) / 256, 1 << 16);
-  hipLaunchKernelGGL(for_each_kernel<F>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, n,
-                     fence, f);
+  hipLaunchKernelGGL(for_each_kernel<F>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, n, f);
   gpu_check_launch("long_glue", s);
 }
 
@@ -65,7 +62,6 @@ struct PassArgs {
   int n1, n2;
   long long stride;  // work buffer line stride
   int blocksPerLine;  // tiles per line tile: ceil(n2 / (B / lt)) (cols), ceil(n1 / (B / lt)) (rows)
-  int fence;  // rows pass: release its stores system-wide at exit (peer-write exchange)
   int lt;     // lines per tile (a power of two dividing B)
   long long lines;
 };
@@ -367,7 +363,6 @@ __device__ __forceinline__ void long_rows_body(const Eng& eng, const PassArgs& a
     const long long line = l0 + (b & (lt - 1));
     if (k1 < a.n1 && line < a.lines) dst(line, k1 + a.n1 * k2, lds[eng.out_at(b, k2)]);
   }
-  release_remote(a.fence);
 }
 template <class Eng, typename T, typename BT, int S>
 __global__ void __launch_bounds__(Eng::kBlock)
@@ -419,7 +414,7 @@ inline void with_long_engine(int n, F&& f) {
 // output for it.
 template <typename T, typename BT, int S>
 void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<T>* work,
-               cx<T>* scratch, hipStream_t stream, int fence = 0) {
+               cx<T>* scratch, hipStream_t stream) {
   if (lines <= 0) return;
   const long long stride = static_cast<long long>(lp.n1) * lp.n2;
   const bool ct1 = long_ct_factor(lp.n1), ct2 = long_ct_factor(lp.n2);
@@ -437,7 +432,7 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
   const bool xStore = io.sk == LongIO<T, BT>::kXPut;
   with_long_engine<T, S>(lp.n1, [&](auto eng, int threads, int B, std::size_t lds) {
     const int lt = decltype(eng)::kBatchedCopy ? 1 : tile(B, xLoad);
-    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n2, B / lt)), 0, lt, lines};
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n2, B / lt)), lt, lines};
     const dim3 grid(static_cast<unsigned>(ceil_div(lines, lt) * a.blocksPerLine));
     const auto* tw1 = static_cast<const cx<T>*>(lp.tw1);
     const auto* twM = static_cast<const cx<T>*>(lp.twM);
@@ -454,8 +449,7 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
   });
   with_long_engine<T, S>(lp.n2, [&](auto eng, int threads, int B, std::size_t lds) {
     const int lt = decltype(eng)::kBatchedCopy ? 1 : tile(B, xStore);
-    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n1, B / lt)), ct2 ? fence : 0, lt,
-               lines};
+    PassArgs a{lp.n1, lp.n2, stride, static_cast<int>(ceil_div(lp.n1, B / lt)), lt, lines};
     const dim3 grid(static_cast<unsigned>(ceil_div(lines, lt) * a.blocksPerLine));
     const auto* tw2 = static_cast<const cx<T>*>(lp.tw2);
     if constexpr (decltype(eng)::kBatchedCopy) {
@@ -475,7 +469,7 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
     for_each(lines * stride, stream, [=] __device__(long long i) {
       const long long line = i / stride;
       l.store(line, static_cast<int>(i - line * stride), res[i]);
-    }, fence);
+    });
   }
 }
 
@@ -486,9 +480,9 @@ void four_step(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cx<
 // 1/m into the second rows pass's stores: four kernels, no glue.
 template <typename T, typename BT, int S>
 void long_fft(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, const LongBufs<T>& w,
-              hipStream_t stream, int fence = 0) {
+              hipStream_t stream) {
   if (!lp.bluestein) {
-    four_step<T, BT, S>(lp, lines, io, w.in, w.out, stream, fence);
+    four_step<T, BT, S>(lp, lines, io, w.in, w.out, stream);
     return;
   }
   const int m = lp.m;
@@ -512,7 +506,7 @@ void long_fft(const LongPlan& lp, long long lines, const LongIO<T, BT>& io, cons
   second.chirpN = lp.n;
   second.chirpConj = S < 0 ? 0 : 1;
   second.outScale = T(1) / static_cast<T>(m);
-  four_step<T, BT, +1>(lp, lines, second, w.w2, w.out, stream, fence);
+  four_step<T, BT, +1>(lp, lines, second, w.w2, w.out, stream);
 }
 
 // ------------------------------------------------------------ plans
@@ -685,7 +679,7 @@ void launch_long_z_backward(const LongPlan& lp, const ZArgs& a, const cx<T>* val
     io.desc = a.desc;
     io.values = values;
     io.zeroStick = a.zeroStick;
-    long_fft<T, BT, +1>(lp, S, io, w, stream, a.remote);
+    long_fft<T, BT, +1>(lp, S, io, w, stream);
     return;
   }
   cx<T>* in = w.out;
@@ -709,7 +703,7 @@ void launch_long_z_backward(const LongPlan& lp, const ZArgs& a, const cx<T>* val
   io.lk = LongIO<T, BT>::kPlain;
   io.src = in;
   io.srcStride = n;
-  long_fft<T, BT, +1>(lp, S, io, w, stream, a.remote);
+  long_fft<T, BT, +1>(lp, S, io, w, stream);
 }
 
 template <typename T, typename BT>
@@ -821,7 +815,7 @@ void launch_long_y_forward(const LongPlan& lp, const YArgs& a, cx<T>* inter, BT*
     io.xout = out;
     io.zb = zb;
     io.C = C;
-    long_fft<T, BT, -1>(lp, lines, io, w, stream, a.remote);
+    long_fft<T, BT, -1>(lp, lines, io, w, stream);
     return;
   }
   cx<T>* res = w.out;
@@ -837,7 +831,7 @@ void launch_long_y_forward(const LongPlan& lp, const YArgs& a, cx<T>* inter, BT*
     const cx<T>* line = res + l * n;
     for (int k = co[c]; k < co[c + 1]; ++k)
       out[cb[k] + zb + zz] = cvt<typename BT::value_type>(line[cy[k]]);
-  }, a.remote);
+  });
 }
 
 // ------------------------------------------------------------ x stage

@@ -46,7 +46,6 @@ struct ZArgs {
   // otherwise, per plane z two entries: (base, stride) of its exchange segment,
   // element (stick s, plane z) at base + s * stride (base includes z)
   const long long* zTab;
-  int remote;  // stores reach peers' memory (peer-write exchange): release system-wide at exit
   BatchPtrs batch;
 };
 
@@ -82,7 +81,6 @@ struct YArgs {
   // optional per-column run descriptors (all columns qualify) and their stride
   const ColDesc* colDesc;
   long long colStride;
-  int remote;  // forward stores reach peers' memory: release system-wide at exit
   BatchPtrs batch;
 };
 

@@ -376,13 +376,6 @@ __device__ __forceinline__ void zero_lds(cx<T>* lds, int count) {
   for (int i = threadIdx.x; i < count; i += blockDim.x) lds[i] = czero<T>();
 }
 
-// Peer-write exchange: this wave's stores to other GPUs' memory are written
-// back system-wide before the kernel ends (the barrier kernel that follows
-// publishes them to the receivers).
-__device__ __forceinline__ void release_remote(int remote) {
-  if (remote) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-}
-
 // A workgroup-uniform value materialised in a scalar register at this point:
 // the compiler may not sink its (scalar) load into later branches.
 __device__ __forceinline__ int pin_uniform(int v) {
@@ -717,7 +710,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
     const int s = s0 + b;
     if (s < a.numSticks) st_stream(&out[seg.at(s, pos)], cvt<typename BT::value_type>(v));
   });
-  release_remote(a.remote);
 }
 
 template <class Eng, typename T, typename BT>
@@ -830,7 +822,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
       return (in0 || in1) ? ld_values(&vals[j]) : czero<T>();
     }, store);
   }
-  release_remote(a.remote);
 }
 
 template <class Eng, typename T, typename BT>
@@ -1143,7 +1134,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const long long base = bases[slot++];
       if (base != kNoBase && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
     });
-    release_remote(a.remote);
     return;
   }
   auto store = [&](int b, int pos, cx<T> v) {
@@ -1152,7 +1142,6 @@ __global__ void __launch_bounds__(Eng::kBlock)
   };
   stage_rows(eng, lds, zl, n, rows);
   eng.lds_to_global(lds, tw, store);
-  release_remote(a.remote);
 }
 
 // x stage column lookup: every x of [0, nFreq) holds a column (e.g. a sphere

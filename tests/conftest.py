@@ -7,6 +7,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+# Environment of a subprocess that injects faults: the testing library (the same
+# kernels and host code plus fault injection and test probes) instead of the release
+# library, which reads no SPFFT_FAULT_* switch.
+TESTING_LIB = os.path.join(REPO, "spfft_amd", "_native", "libspfft_amd_testing.so")
+TESTING_ENV = {"SPFFT_AMD_LIBRARY": TESTING_LIB}
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X)")

@@ -276,3 +276,23 @@ def test_bench_model_relay_shares():
     # pipelined grid: all but one step's compute hidden behind the link
     piped = b._model(stages, 52.7e6, 2, 2, 2)
     assert abs(piped["backward"]["predicted_ms"] - (direct["backward"]["link_ms"] + 0.25 / 4)) < 1e-9
+
+
+def test_release_library_has_no_test_hooks():
+    """The release library exports no test probe and reads no fault-injection switch;
+    both live in the testing library only (CMake SPFFT_TESTING_LIBRARY,
+    src/core/fault.hpp, src/testing/)."""
+    import os
+    import shutil
+    import subprocess
+    from conftest import TESTING_LIB
+    from spfft_amd.ops._lib import NATIVE_DIR
+    rel = os.path.join(NATIVE_DIR, "libspfft_amd.so")
+    nm = shutil.which("nm") or "/usr/bin/nm"
+    syms = subprocess.run([nm, "-D", "--defined-only", rel], capture_output=True, text=True, check=True).stdout
+    assert "spfft_amd_test_" not in syms and "shm_check" not in syms
+    with open(rel, "rb") as f:
+        assert b"SPFFT_FAULT_" not in f.read()
+    tsyms = subprocess.run([nm, "-D", "--defined-only", TESTING_LIB], capture_output=True, text=True,
+                           check=True).stdout
+    assert "spfft_amd_test_comm_shm_check" in tsyms and "spfft_amd_test_fault_injection" in tsyms

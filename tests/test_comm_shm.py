@@ -7,21 +7,40 @@ import re
 import subprocess
 import sys
 
-from spfft_amd.parallel.comm import run_ranks
+from conftest import TESTING_ENV
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_shm_collectives_threads():
-    res = run_ranks(4, lambda r, c: c.shm_check(500))
-    for shm, com in res:
-        assert shm is not None and shm > 0 and com > 0
+    """4 in-process ranks (local group) through the testing library's probe."""
+    code = ("from spfft_amd.parallel.comm import run_ranks\n"
+            "res = run_ranks(4, lambda r, c: c.shm_check(500))\n"
+            "assert all(s is not None and s > 0 and c > 0 for s, c in res), res\n"
+            "print('THREADS OK')\n")
+    e = dict(os.environ, OMP_NUM_THREADS="1", **TESTING_ENV)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=e, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "THREADS OK" in r.stdout, (r.stdout + r.stderr)[-4000:]
+
+
+def test_shm_probe_absent_from_release_library():
+    """The probe is not part of the release library's ABI."""
+    code = ("from spfft_amd.parallel.comm import run_ranks\n"
+            "try:\n"
+            "    run_ranks(2, lambda r, c: c.shm_check(5))\n"
+            "except Exception as e:\n"
+            "    print('REFUSED', e)\n")
+    e = {k: v for k, v in os.environ.items() if k != "SPFFT_AMD_LIBRARY"}
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=e, capture_output=True, text=True,
+                       timeout=300)
+    assert "REFUSED" in r.stdout and "testing library" in r.stdout, (r.stdout + r.stderr)[-4000:]
 
 
 def _probe(nproc, env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
            f"--nproc-per-node={nproc}", os.path.join(REPO, "tools", "shm_probe.py"), "--iters", "300"]
-    e = dict(os.environ, OMP_NUM_THREADS="1", **(env or {}))
+    e = dict(os.environ, OMP_NUM_THREADS="1", **TESTING_ENV, **(env or {}))
     r = subprocess.run(cmd, cwd=REPO, env=e, capture_output=True, text=True, timeout=300)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
@@ -56,7 +75,7 @@ def test_shm_peer_exit_detected():
     waits end with an error naming the exited rank (liveness check), not a hang."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
            "--nproc-per-node=2", os.path.join(REPO, "tools", "shm_probe.py"), "--iters", "300"]
-    e = dict(os.environ, OMP_NUM_THREADS="1", SPFFT_FAULT_SHM_EXIT="1")
+    e = dict(os.environ, OMP_NUM_THREADS="1", SPFFT_FAULT_SHM_EXIT="1", **TESTING_ENV)
     r = subprocess.run(cmd, cwd=REPO, env=e, capture_output=True, text=True, timeout=120)
     out = r.stdout + r.stderr
     assert "SHM ERROR rank=0" in out and "has exited" in out, out[-4000:]

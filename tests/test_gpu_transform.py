@@ -1,11 +1,15 @@
 """GPU numerics: the hand-written HIP stage kernels against fp64 references
 (numpy for small sizes, torch.fft on the GPU for large ones)."""
+import os
+
 import numpy as np
 import pytest
 
 import spfft_amd as sp
 from spfft_amd.utils.indices import (center_indices, create_value_indices, sphere_indices)
 from spfft_amd.utils.oracle import dense_backward, dense_forward, max_rel_error
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -972,38 +976,18 @@ def test_rccl_channel_shared_across_grids(gpu, monkeypatch):
     assert 0 <= sp.rccl_communicators() - before <= P
 
 
-def test_rccl_abort_is_reported(gpu, monkeypatch):
+def test_rccl_abort_is_reported(gpu):
     """Failure detection on the RCCL plane: the 2nd exchange aborts the communicator
-    (ncclCommAbort on a live RCCL communicator, SPFFT_FAULT_EXCHANGE_ABORT=2); that
-    call and every later exchange raise MPIError instead of hanging."""
-    import torch
-    from spfft_amd.parallel import make_distributed, run_ranks
-    monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
-    monkeypatch.setenv("SPFFT_RCCL_SHARE", "0")
-    monkeypatch.setenv("SPFFT_FAULT_EXCHANGE_ABORT", "2")
-    dims = (16, 12, 10)
-    gidx = sphere_indices(*dims, 0.5)
-    from spfft_amd.utils.indices import distribute_sticks
-    parts = distribute_sticks(gidx, 2, dims)
-
-    def body(rank, comm):
-        torch.cuda.set_device(0)
-        s = make_distributed(comm, dims, gidx, processing_unit=GPU)
-        start = sum(len(p) for p in parts[:rank])
-        v = torch.ones(len(s.indices), dtype=torch.complex128, device="cuda")
-        s.transform.backward(v)  # exchange 1: fine
-        msgs = []
-        for _ in range(2):
-            try:
-                s.transform.forward(None)
-                msgs.append(None)
-            except sp.MPIError as err:
-                msgs.append(str(err))
-        del start
-        return msgs
-
-    for msgs in run_ranks(2, body):
-        assert all(m is not None and "abort" in m for m in msgs), msgs
+    (ncclCommAbort on a live RCCL communicator, fault injection EXCHANGE_ABORT=2 of the
+    testing library); that call and every later exchange raise MPIError instead of
+    hanging (tools/fault_rccl_abort.py, in its own process)."""
+    import subprocess
+    import sys
+    from conftest import TESTING_ENV
+    e = dict(os.environ, **TESTING_ENV)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "fault_rccl_abort.py")], cwd=REPO, env=e,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ABORT OK" in r.stdout, (r.stdout + r.stderr)[-4000:]
 
 
 @pytest.mark.parametrize("ttype", ["c2c", "r2c"])

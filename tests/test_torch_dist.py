@@ -17,6 +17,8 @@ import sys
 
 import pytest
 
+from conftest import TESTING_ENV, TESTING_LIB
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROBE = os.path.join(REPO, "tools", "rccl_probe.py")
 
@@ -90,6 +92,7 @@ def test_rccl_init_failure_falls_back_to_peer_writes(gpu, monkeypatch):
     """Fault injection: every rank's RCCL initialisation fails. The ranks agree on
     the outcome (allgather) and move the exchange with IPC peer writes instead."""
     monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "1")
+    monkeypatch.setenv("SPFFT_AMD_LIBRARY", TESTING_LIB)
     _launch(2, "COMPACT_BUFFERED", "--iters=2", expect="ipc")
 
 
@@ -100,6 +103,7 @@ def test_rccl_init_failure_one_rank(gpu, monkeypatch):
     until SPFFT_COMM_TIMEOUT, aborts, and both ranks agree on the peer-write fallback
     instead of one of them blocking inside RCCL."""
     monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "2")
+    monkeypatch.setenv("SPFFT_AMD_LIBRARY", TESTING_LIB)
     monkeypatch.setenv("SPFFT_COMM_TIMEOUT", "5")
     _launch(2, "COMPACT_BUFFERED", "--iters=2", expect="ipc", timeout=180)
 
@@ -109,6 +113,7 @@ def test_rccl_init_failure_strict(gpu, monkeypatch):
     """With SPFFT_GPU_EXCHANGE=rccl there is no fallback: every rank raises MPIError
     (with the cause) instead of hanging."""
     monkeypatch.setenv("SPFFT_FAULT_RCCL_INIT", "1")
+    monkeypatch.setenv("SPFFT_AMD_LIBRARY", TESTING_LIB)
     monkeypatch.setenv("SPFFT_GPU_EXCHANGE", "rccl")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", PROBE, "COMPACT_BUFFERED"]
@@ -116,7 +121,7 @@ def test_rccl_init_failure_strict(gpu, monkeypatch):
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     out = r.stdout + r.stderr
     assert r.returncode != 0, out[-4000:]
-    assert "MPIError" in out and "SPFFT_FAULT_RCCL_INIT" in out, out[-4000:]
+    assert "MPIError" in out and "fault injection RCCL_INIT" in out, out[-4000:]
 
 
 def _bench_json(out):
@@ -265,8 +270,8 @@ def test_ipc_peer_self_test_failure_detected(gpu):
     message to rank 0) fails the plane on every rank. Ranks that share one GPU have no
     other plane (RCCL refuses them), so grid setup raises MPIError everywhere; ranks
     on distinct GPUs fall back to RCCL (DeviceComm::create)."""
-    code, out = _launch_tool(2, "rccl_probe.py", "UNBUFFERED", env_extra={"SPFFT_FAULT_PEER_SELFTEST": "1"},
-                             timeout=180)
+    code, out = _launch_tool(2, "rccl_probe.py", "UNBUFFERED",
+                             env_extra={"SPFFT_FAULT_PEER_SELFTEST": "1", **TESTING_ENV}, timeout=180)
     assert code != 0, out[-4000:]
     assert out.count("route self-test failed") >= 2, out[-4000:]
 
@@ -277,7 +282,7 @@ def test_ipc_stale_mapping_detected(gpu, monkeypatch):
     injection: the last rank announces a wrong one) is reported as MPIError on
     every rank at grid setup; nothing is computed on it."""
     code, out = _launch_tool(2, "rccl_probe.py", "UNBUFFERED",
-                             env_extra={"SPFFT_FAULT_IPC_NONCE": "1"}, timeout=180)
+                             env_extra={"SPFFT_FAULT_IPC_NONCE": "1", **TESTING_ENV}, timeout=180)
     assert code != 0, out[-4000:]
     assert out.count("stale IPC mapping") >= 2, out[-4000:]
 
@@ -360,6 +365,7 @@ def test_relay_self_test_failure_falls_back(gpu, monkeypatch):
     printed once."""
     monkeypatch.setenv("SPFFT_RELAY", "force")
     monkeypatch.setenv("SPFFT_FAULT_RELAY_SELFTEST", "1")
+    monkeypatch.setenv("SPFFT_AMD_LIBRARY", TESTING_LIB)
     code, out = _launch_tool(2, "rccl_probe.py", "COMPACT_BUFFERED", "--iters=2")
     assert code == 0, out[-4000:]
     assert out.count("[ipc]") == 2 and "self-test exchange delivered wrong data" in out, out[-4000:]

@@ -9,7 +9,10 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+# the probe lives in the testing library (not in the release ABI)
+os.environ.setdefault("SPFFT_AMD_LIBRARY", os.path.join(REPO, "spfft_amd", "_native", "libspfft_amd_testing.so"))
 
 
 def main():
@@ -24,7 +27,7 @@ def main():
     try:
         shm, com = comm.shm_check(args.iters)
     except Exception as e:  # noqa: BLE001
-        # (SPFFT_FAULT_SHM_EXIT: a peer left; the wait must end with an error)
+        # (fault injection SHM_EXIT: a peer left; the wait must end with an error)
         print(f"SHM ERROR rank={dist.get_rank()} {e}", flush=True)
         os._exit(0)
     print(f"SHM OK rank={dist.get_rank()} " + json.dumps({"shm_us": shm, "comm_us": com}), flush=True)
