@@ -125,6 +125,16 @@ SPFFT_EXPORT SpfftError spfft_amd_transform_backward_z(SpfftTransform t, const d
 SPFFT_EXPORT SpfftError spfft_amd_transform_backward_exchange(SpfftTransform t, int nonBlocking);
 SPFFT_EXPORT SpfftError spfft_amd_transform_backward_xy(SpfftTransform t,
                                                         SpfftProcessingUnitType outputLocation);
+/* The same steps for single precision transforms. */
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_forward_xy(SpfftFloatTransform t,
+                                                             SpfftProcessingUnitType inputLocation);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_forward_exchange(SpfftFloatTransform t, int nonBlocking);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_forward_z(SpfftFloatTransform t, float* output,
+                                                            SpfftScalingType scaling);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_backward_z(SpfftFloatTransform t, const float* input);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_backward_exchange(SpfftFloatTransform t, int nonBlocking);
+SPFFT_EXPORT SpfftError spfft_amd_float_transform_backward_xy(SpfftFloatTransform t,
+                                                              SpfftProcessingUnitType outputLocation);
 
 /* Timer tree (SPFFT_TIMING=1 or spfft_amd_timing_enable). enable: 0 off, 1 host
  * scopes only (like the reference's timer), 2 host scopes and GPU stage times

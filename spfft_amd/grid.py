@@ -224,6 +224,7 @@ class _TransformBase:
         self._stream = None
         self._cache = {}
         self._views = {}
+        self._step_keep = None
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -364,6 +365,41 @@ class _TransformBase:
 
     def synchronize(self):
         _check(self._prec.amd_fn("transform_synchronize")(self._h))
+
+    # Step-wise execution (spfft/amd.h): backward = backward_z, backward_exchange,
+    # backward_xy; forward = forward_xy, forward_exchange, forward_z. Every rank calls
+    # the same steps in the same order (the exchanges are collective); work that does
+    # not depend on the exchange can be placed between the steps.
+    def backward_z(self, values):
+        ptr, keep = _data_ptr(values, self._prec, False, "values")
+        _check(self._prec.amd_fn("transform_backward_z")(self._h, ptr))
+        self._step_keep = keep  # until the next step: the z stage may still read it
+
+    def backward_exchange(self, non_blocking: bool = False):
+        _check(self._prec.amd_fn("transform_backward_exchange")(self._h, 1 if non_blocking else 0))
+
+    def backward_xy(self, output_location=None):
+        if output_location is None:
+            output_location = self.processing_unit
+        _check(self._prec.amd_fn("transform_backward_xy")(self._h, int(output_location)))
+        self._step_keep = None
+        return self.space_domain(output_location)
+
+    def forward_xy(self, input_location=None):
+        if input_location is None:
+            input_location = self.processing_unit
+        _check(self._prec.amd_fn("transform_forward_xy")(self._h, int(input_location)))
+
+    def forward_exchange(self, non_blocking: bool = False):
+        _check(self._prec.amd_fn("transform_forward_exchange")(self._h, 1 if non_blocking else 0))
+
+    def forward_z(self, output=None, scaling=Scaling.NONE):
+        if output is None:
+            output = self._default_output()
+        ptr, keep = _data_ptr(output, self._prec, True, "output")
+        _check(self._prec.amd_fn("transform_forward_z")(self._h, ptr, int(scaling)))
+        self._step_keep = keep
+        return output
 
     def exchange_plan(self):
         """(plane chunks K, stick blocks I, peer writes, relay GPUs) of the GPU exchange."""

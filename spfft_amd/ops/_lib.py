@@ -112,6 +112,12 @@ def _prototypes(lib):
     sig["spfft_amd_transform_backward_z"] = [V, D]
     sig["spfft_amd_transform_backward_exchange"] = [V, I]
     sig["spfft_amd_transform_backward_xy"] = [V, I]
+    sig["spfft_amd_float_transform_forward_xy"] = [V, I]
+    sig["spfft_amd_float_transform_forward_exchange"] = [V, I]
+    sig["spfft_amd_float_transform_forward_z"] = [V, D, I]
+    sig["spfft_amd_float_transform_backward_z"] = [V, D]
+    sig["spfft_amd_float_transform_backward_exchange"] = [V, I]
+    sig["spfft_amd_float_transform_backward_xy"] = [V, I]
     sig["spfft_amd_timing_enable"] = [I]
     sig["spfft_amd_timing_reset"] = []
     sig["spfft_amd_timing_json"] = [ctypes.c_char_p, ctypes.c_size_t, c_size_t_p]

@@ -481,6 +481,25 @@ SpfftError spfft_amd_transform_backward_exchange(SpfftTransform t, int nonBlocki
 SpfftError spfft_amd_transform_backward_xy(SpfftTransform t, SpfftProcessingUnitType loc) {
   return with_handle<Transform>(t, [&](Transform& x) { x.backward_xy(loc); });
 }
+SpfftError spfft_amd_float_transform_forward_xy(SpfftFloatTransform t, SpfftProcessingUnitType loc) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.forward_xy(loc); });
+}
+SpfftError spfft_amd_float_transform_forward_exchange(SpfftFloatTransform t, int nonBlocking) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.forward_exchange(nonBlocking != 0); });
+}
+SpfftError spfft_amd_float_transform_forward_z(SpfftFloatTransform t, float* output,
+                                               SpfftScalingType scaling) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.forward_z(output, scaling); });
+}
+SpfftError spfft_amd_float_transform_backward_z(SpfftFloatTransform t, const float* input) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.backward_z(input); });
+}
+SpfftError spfft_amd_float_transform_backward_exchange(SpfftFloatTransform t, int nonBlocking) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.backward_exchange(nonBlocking != 0); });
+}
+SpfftError spfft_amd_float_transform_backward_xy(SpfftFloatTransform t, SpfftProcessingUnitType loc) {
+  return with_handle<TransformFloat>(t, [&](TransformFloat& x) { x.backward_xy(loc); });
+}
 
 SpfftError spfft_amd_timing_enable(int enable) {
   timing::set_level(enable);

@@ -1204,3 +1204,40 @@ def test_peer_write_offsets_both_signs(gpu, monkeypatch, capfd):
     ranges = [(int(a), int(b)) for a, b in re.findall(r"peer_offsets=\[(-?\d+), (-?\d+)\]", err)]
     assert len(ranges) == 3, err[-2000:]
     assert min(r[0] for r in ranges) < 0 < max(r[1] for r in ranges), ranges
+
+
+@pytest.mark.parametrize("single", [False, True])
+def test_grid_host_and_gpu(gpu, single):
+    """A grid created with SPFFT_PU_HOST | SPFFT_PU_GPU holds both memories and serves a
+    HOST transform and a GPU transform (reference: grid_internal.cpp:60-77,
+    transform_internal.cpp:69-77); both match the dense oracle, and the GPU transform's
+    host-located output matches too."""
+    import torch
+    dims = (24, 20, 18)
+    nx, ny, nz = dims
+    rng = np.random.default_rng(11)
+    idx = create_value_indices(rng, [1.0], 0.6, 0.8, nx, ny, nz, False)[0]
+    vals = rng.standard_normal(len(idx)) + 1j * rng.standard_normal(len(idx))
+    ref = dense_backward(idx, vals, dims)
+    G = sp.GridFloat if single else sp.Grid
+    cdt = np.complex64 if single else np.complex128
+    tol = 2e-5 if single else 1e-12
+    both = int(sp.ProcessingUnit.HOST) | int(sp.ProcessingUnit.GPU)
+    grid = G(nx, ny, nz, nx * ny, both, 2)
+    th = grid.create_transform(sp.ProcessingUnit.HOST, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    tg = grid.create_transform(sp.ProcessingUnit.GPU, sp.TransformType.C2C, nx, ny, nz, nz, idx)
+    v = vals.astype(cdt)
+    assert max_rel_error(np.array(th.backward(v)), ref) < tol
+    out = tg.backward(torch.as_tensor(v, device="cuda"))
+    torch.cuda.synchronize()
+    assert max_rel_error(out.cpu().numpy(), ref) < tol
+    # GPU transform, output in host memory
+    hout = tg.backward(torch.as_tensor(v, device="cuda"), output_location=sp.ProcessingUnit.HOST)
+    assert max_rel_error(np.array(hout), ref) < tol
+    # forward of both from their own space domains
+    space = (rng.standard_normal((nz, ny, nx)) + 1j * rng.standard_normal((nz, ny, nx))).astype(cdt)
+    fref = dense_forward(space.astype(np.complex128), idx, dims)
+    assert max_rel_error(np.array(th.forward(space)), fref) < tol * 10
+    fg = tg.forward(torch.as_tensor(space, device="cuda"))
+    torch.cuda.synchronize()
+    assert max_rel_error(fg.cpu().numpy(), fref) < tol * 10
