@@ -36,32 +36,32 @@ sys.path.insert(0, REPO)
 REF_FFT_ONLY_256_BY_T = {1: 2210.2, 4: 2418.3}  # profiles/r3/comparator/
 
 # xGMI bandwidth one peer pair gets per direction (one link of an MI355X node:
-# 153.6 GB/s per link both directions, ~70 GB/s usable one way), the model's
-# assumption until the driver's N = 2/4/8 runs measure it
+# 153.6 GB/s per link both directions, ~70 GB/s usable one way): the model's
+# assumption when the data plane has not measured it (plane info
+# "link_GBps_measured": an 8 MiB copy into every rank's right neighbour at setup)
 LINK_GBPS = 70.0
-# host round trips of one relay-plane exchange (two stream synchronisations and the
-# node-local shared-memory collectives; profiles/r5/relay/overhead.txt)
-RELAY_HOST_MS = 0.06
+# two device barrier rounds per relay exchange (stream-ordered relay plane)
+RELAY_BARRIER_MS = 0.02
 
 
-def _model(stages, sent_per_rank, world, chunks, blocks, relays=0):
+def _model(stages, sent_per_rank, world, chunks, blocks, relays=0, link_gbps=None):
     """Modelled per-direction times of a distributed step (README, "Multi-GPU
     scaling"): every rank sends sent/(N-1) bytes to each peer over its own link, all
-    links at once, so the exchange takes link_ms = sent/(N-1) / LINK_GBPS; the
+    links at once, so the exchange takes link_ms = sent/(N-1) / link rate; the
     compute is this run's own z and y/x stage times. The pipelined grid of K plane
     chunks x I stick blocks overlaps all but one step's compute with the link:
     predicted = max(link, compute) + compute / (K * I) (unpipelined: link + compute).
     The driver's measured ms_per_step / (2 T) can be read against `predicted_ms`."""
+    rate = link_gbps if link_gbps else LINK_GBPS
     per_peer = sent_per_rank / max(1, world - 1)
     # relay plane: every link direction carries (N - 1) / (N - 1 + K) of a
-    # peer message, in two host-synchronous hops (push, pull)
+    # peer message, in two stream-ordered hops (push, pull)
     share = (world - 1) / (world - 1 + relays) if relays else 1.0
-    link_ms = per_peer * share / (LINK_GBPS * 1e9) * 1e3 * (2 if relays else 1)
-    link_ms += RELAY_HOST_MS if relays else 0.0
-    out = {"link_GBps_assumed": LINK_GBPS, "bytes_per_peer": per_peer,
+    link_ms = per_peer * share / (rate * 1e9) * 1e3 * (2 if relays else 1)
+    link_ms += RELAY_BARRIER_MS if relays else 0.0
+    out = {"link_GBps_assumed": LINK_GBPS, "link_GBps_used": rate,
+           "link_GBps_source": "measured" if link_gbps else "assumed", "bytes_per_peer": per_peer,
            "chunks": chunks, "stick_blocks": blocks, "relay_gpus": relays}
-    if relays:
-        out["relay_host_ms"] = RELAY_HOST_MS
     for d in ("backward", "forward"):
         st = stages.get(d, {})
         compute = sum(v for k, v in st.items() if k not in ("exchange", "exchange-span", "exchange-tail", "total"))
@@ -103,6 +103,10 @@ def parse():
     ap.add_argument("--profile-reps", type=int, default=5,
                     help="backward+forward pairs of transform 0 timed per stage after the "
                          "timed loop (0 = no stage profile)")
+    ap.add_argument("--planes-probe", type=int, default=1,
+                    help="N > 1: after the timed loop, time a few steps (one transform per step) on "
+                         "every eligible data plane (rccl / ipc / relay) and record them in "
+                         "config.planes_ms; the headline stays on the default plane")
     ap.add_argument("--sync", default="stream", choices=["stream", "call"],
                     help="stream: transforms are stream-ordered on torch's current stream (no host "
                          "wait per call; the timed loop still ends with a device synchronize); "
@@ -142,6 +146,56 @@ def _roundtrip_gpu(sp, ts, vals, outs, r2c):
         scale = float(base.abs().max().item()) or 1.0
         worst = max(worst, float((o - base).abs().max().item()) / scale)
     return worst
+
+
+def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, warmup=2):
+    """ms per step (one backward + forward of one transform) on every eligible data
+    plane, each forced through the library's plane switches (read at grid setup):
+    rccl (not between ranks that share a GPU), ipc (peer writes) and relay (idle GPUs
+    of the node, or virtual relays on a shared GPU). A plane the library cannot set up
+    is recorded with its error (the failure is agreed on by every rank)."""
+    import time as _t
+    import torch
+    planes = {"rccl": {"SPFFT_GPU_EXCHANGE": "rccl", "SPFFT_RELAY": "0"},
+              "ipc": {"SPFFT_GPU_EXCHANGE": "ipc", "SPFFT_RELAY": "0"},
+              "relay": {"SPFFT_GPU_EXCHANGE": "", "SPFFT_RELAY": "force" if shared else "auto"}}
+    out = {}
+    for name, env in planes.items():
+        if name == "rccl" and shared:
+            out[name] = {"skipped": "ranks share a GPU (RCCL refuses duplicate devices)"}
+            continue
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        g = t = None
+        try:
+            g, t, local, _ = make_transform()
+            t.set_stream(torch.cuda.current_stream(), synchronous=False)
+            v = torch.randn(len(local), dtype=cdtype, device=dev)
+            o = torch.empty_like(v)
+            for _ in range(warmup):
+                t.backward(v)
+                t.forward(None, output=o)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = _t.perf_counter()
+            for _ in range(steps):
+                t.backward(v)
+                t.forward(None, output=o)
+            torch.cuda.synchronize()
+            e = torch.tensor([_t.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            out[name] = {"ms_per_step": 1e3 * float(e.item()) / steps, "plane": g.data_plane}
+        except Exception as ex:  # noqa: BLE001 - recorded
+            out[name] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        finally:
+            for k, val in saved.items():
+                if val is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = val
+            del t, g
+            torch.cuda.synchronize()
+    return out
 
 
 def _timing_node(tree, path):
@@ -327,7 +381,7 @@ def main():
         check.update(_check(a, sp, t, values, gidx, dims, ttype, world))
     # per-direction stage times of transform 0 alone, and the exchange rate
     stages = _stage_profile(sp, t, values, out, a.profile_reps) if a.profile_reps > 0 else {}
-    exch = None
+    xstats = None
     if world > 1 and stages:
         eb = (8 if single or "Float" in a.exchange else 16)
         loc = np.asarray(local).reshape(-1, 3).astype(np.int64)
@@ -338,21 +392,25 @@ def main():
         for d in ("backward", "forward"):
             st = stages.get(d, {})
             ms[d] = st.get("exchange-span", st.get("exchange"))
-        exch = {"bytes_sent_per_rank": sent,
+        xstats = {"bytes_sent_per_rank": sent,
                 "ms": ms,
                 "GBps_per_rank": {d: (sent / (v * 1e-3) / 1e9 if v else None) for d, v in ms.items()}}
         e = torch.tensor([float(sent)], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        exch["max_bytes_sent_per_rank"] = float(e.item())
+        xstats["max_bytes_sent_per_rank"] = float(e.item())
     # ranks that share a device (rehearsal on a small box) are not a multi-GPU
     # measurement: record how many distinct devices the ranks ran on
     n_devices = len(set(rank_devs))
     model = None
     if world > 1 and stages:
         chunks, blocks, peer_writes, relays = t.exchange_plan()
-        model = _model(stages, exch["max_bytes_sent_per_rank"], world, chunks, blocks, relays)
+        model = _model(stages, xstats["max_bytes_sent_per_rank"], world, chunks, blocks, relays,
+                       plane_info.get("link_GBps_measured"))
         model["peer_writes"] = peer_writes
         model["shared_device"] = n_devices < world
+    planes_ms = None
+    if world > 1 and a.planes_probe:
+        planes_ms = _probe_planes(make_transform, dev, cdtype, world, n_devices < world, dist)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * T * a.steps / elapsed
     # the reference's FFT calls alone (rocFFT via
@@ -404,8 +462,12 @@ def main():
                 "stage_ms": stages,
                 "stage_ms_basis": (f"transform 0 alone, median of {a.profile_reps} backward+forward "
                                    "pairs after the timed loop (hipEvent stage marks)" if stages else None),
-                "exchange_stats": exch,
+                "exchange_stats": xstats,
                 "model_ms": model,
+                "planes_ms": planes_ms,
+                "planes_ms_basis": ("one transform per step, 2 warmup + 5 timed steps per plane after "
+                                    "the timed loop; the headline uses the default plane"
+                                    if planes_ms else None),
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),
             },

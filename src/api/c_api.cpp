@@ -137,7 +137,7 @@ const char* data_plane_info_of(Impl& impl) {
   if (!(impl.processing_unit() & SPFFT_PU_GPU) || impl.local())
     buf = "{\"kind\": \"none\"}";
   else
-    buf = impl.device_comm().info_json();
+    buf = impl.device_comm().info();
   return buf.c_str();
 }
 }  // namespace

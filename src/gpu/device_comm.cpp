@@ -15,6 +15,7 @@
 #include <random>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "core/common.hpp"
@@ -945,6 +946,128 @@ private:
   std::vector<std::string> devices_;  // every rank's GPU (PCI location)
 };
 
+// ------------------------------------------------- stream-ordered barriers
+// The barrier rounds of a cross-process data plane (peer_sync.hip) with flag
+// arrays of its own: leased from the IPC arena (uncached), mapped by every
+// rank, one epoch per round. Used by the relay plane; setup and teardown are
+// collective and agree on failure (every rank throws MPIError together).
+struct BarrierRounds {
+  int device = 0, me = 0, P = 1;
+  unsigned* failHost = nullptr;
+  unsigned* failDev = nullptr;
+  std::unique_ptr<IpcLease> flags;
+  std::vector<void*> opened;
+  std::unique_ptr<DeviceBuffer> table;
+  unsigned long long epoch = 0;
+  long long timeoutTicks = 0;
+  unsigned xcdMask = 0;
+
+  void setup(Communicator& comm, int dev) {
+    device = dev;
+    me = comm.rank();
+    P = comm.size();
+    DeviceGuard guard(device);
+    gpu_check(hipHostMalloc(reinterpret_cast<void**>(&failHost), 64, hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc");
+    *failHost = 0;
+    gpu_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&failDev), failHost, 0), "hipHostGetDevicePointer");
+    xcdMask = dev::xcd_mask(device);
+    int rateKHz = 0;
+    gpu_check(hipDeviceGetAttribute(&rateKHz, hipDeviceAttributeWallClockRate, device), "hipDeviceGetAttribute");
+    const char* env = std::getenv("SPFFT_PEER_TIMEOUT");
+    const double seconds = env && *env ? std::max(0.1, std::atof(env)) : 30.0;
+    timeoutTicks = static_cast<long long>(seconds * 1e3 * std::max(rateKHz, 1));
+    struct Outcome {
+      int ok;
+      char why[160];
+    };
+    Outcome res{1, {0}};
+    IpcExport mine{};
+    const std::size_t fbytes = static_cast<std::size_t>(dev::peer_flag_words(P)) * 8;
+    try {
+      flags = ipc_acquire(device, fbytes, true);
+      gpu_check(hipMemset(flags->data(), 0, fbytes), "hipMemset");
+      mine = flags->describe();
+    } catch (const std::exception& ex) {
+      res.ok = 0;
+      std::snprintf(res.why, sizeof(res.why), "barrier flags: %s", ex.what());
+    }
+    std::vector<IpcExport> all(P);
+    comm.allgather(&mine, all.data(), sizeof(IpcExport));
+    std::vector<unsigned long long*> tab(P, nullptr);
+    if (res.ok) {
+      try {
+        for (int q = 0; q < P && res.ok; ++q) {
+          if (q == me) {
+            tab[q] = static_cast<unsigned long long*>(flags->data());
+            continue;
+          }
+          std::string why;
+          void* p = all[q].valid ? ipc_open_checked(all[q], &why) : nullptr;
+          if (!p) {
+            res.ok = 0;
+            std::snprintf(res.why, sizeof(res.why), "flags of rank %d: %s", q,
+                          all[q].valid ? why.c_str() : "not announced");
+            break;
+          }
+          opened.push_back(p);
+          tab[q] = static_cast<unsigned long long*>(p);
+        }
+        if (res.ok) {
+          table.reset(new DeviceBuffer(sizeof(void*) * P));
+          gpu_check(hipMemcpy(table->data(), tab.data(), sizeof(void*) * P, hipMemcpyHostToDevice), "hipMemcpy");
+        }
+      } catch (const std::exception& ex) {
+        res.ok = 0;
+        std::snprintf(res.why, sizeof(res.why), "barrier flags: %s", ex.what());
+      }
+    }
+    std::vector<Outcome> outs(P);
+    comm.allgather(&res, outs.data(), sizeof(Outcome));
+    for (const Outcome& o : outs)
+      if (!o.ok) {
+        release();
+        set_error_detail(std::string("data plane barrier setup: ") + o.why);
+        throw MPIError();
+      }
+    gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    comm.barrier();  // every flag array is zeroed before the first round
+  }
+  // one round on `stream` (the caller keeps every round of the plane on one stream)
+  void round(hipStream_t stream) {
+    dev::launch_peer_barrier(table->data<unsigned long long*>(), static_cast<unsigned long long*>(flags->data()),
+                             me, P, ++epoch, failDev, timeoutTicks, xcdMask, stream);
+  }
+  bool healthy(std::string* detail) const {
+    const unsigned f = failHost ? __atomic_load_n(failHost, __ATOMIC_ACQUIRE) : 0u;
+    if (f == 0) return true;
+    if (detail) {
+      if (f & 2u)
+        *detail = "data plane barrier: aborted (host-side timeout or an earlier failure)";
+      else if (f & 1u)
+        *detail = "data plane barrier: a rank did not arrive within SPFFT_PEER_TIMEOUT";
+      else if (f & dev::kPeerXcdMiss)
+        *detail = "data plane barrier: a round's workgroups did not run on every XCD";
+      else
+        *detail = "data plane barrier: a peer rank gave up waiting";
+    }
+    return false;
+  }
+  void abort() {
+    if (failHost) __atomic_fetch_or(failHost, 2u, __ATOMIC_ACQ_REL);
+  }
+  void release() {
+    for (void* p : opened) ipc_close(p);
+    opened.clear();
+  }
+  ~BarrierRounds() {
+    if (process_exiting()) return;
+    release();
+    if (failHost && __atomic_load_n(failHost, __ATOMIC_ACQUIRE) != 0 && flags) flags->discard();
+    if (failHost) (void)hipHostFree(failHost);
+  }
+};
+
 // ------------------------------------------------------------ relay routing
 // Ranks on distinct GPUs of one node that leave other GPUs of the node idle
 // (the driver's N = 2 and N = 4 runs on an 8-GPU node): every peer message is
@@ -978,7 +1101,7 @@ private:
 class RelayDeviceComm : public DeviceComm {
 public:
   RelayDeviceComm(const std::shared_ptr<Communicator>& comm, int device, const std::size_t bytes[2],
-                  const std::vector<int>& relayDevices)
+                  const std::vector<int>& relayDevices, const std::string& channelKey)
       : comm_(comm), device_(device), me_(comm->rank()), P_(comm->size()),
         K_(static_cast<int>(relayDevices.size())), relayDev_(relayDevices) {
     DeviceGuard guard(device);
@@ -1077,13 +1200,20 @@ public:
       set_error_detail(std::string("relay data plane: ") + o.why);
       throw MPIError();
     }
-    const std::size_t maxSegs = static_cast<std::size_t>(2 * P_ + 2) * (1 + K_) + 8;
-    segsHost_.resize(maxSegs);
-    segsDev_.reset(new DeviceBuffer(maxSegs * sizeof(dev::CopySeg)));
     gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    // device barrier rounds and the plane's stream (registered exchanges)
+    bar_.setup(*comm_, device);
+    // one ordered stream per member set and device, shared by every relay
+    // plane of the process: the barrier rounds of all its grids run in host
+    // issue order, the order every rank issues them in (transforms are
+    // collective), whatever hardware queue the stream lands on
+    channel_ = acquire_peer_channel(channelKey, device);
+    gpu_check(hipEventCreateWithFlags(&evIn_, hipEventDisableTiming), "hipEventCreateWithFlags");
+    gpu_check(hipEventCreateWithFlags(&evOut_, hipEventDisableTiming), "hipEventCreateWithFlags");
     // the per-exchange host collectives (one allgather, two barriers) through
     // shared memory when every rank maps the segment, else through comm
-    shm_ = ShmGroup::create(*comm_, sizeof(Transfer) * static_cast<std::size_t>(2 * P_ + 1), comm_timeout_seconds());
+    shmPayload_ = sizeof(Transfer) * static_cast<std::size_t>(2 * P_ + 1);
+    shm_ = ShmGroup::create(*comm_, shmPayload_, comm_timeout_seconds());
     devices_ = group_devices(*comm_, device);
     for (int c : relayDev_) devices_.push_back(pci_string(pci_of(c)));
     comm_->barrier();
@@ -1121,11 +1251,16 @@ public:
       gpu_check(hipMemset(recv, 0, pattern.size() * 8), "hipMemset");
       std::vector<std::int64_t> cnt(P_, per), dsp(P_);
       for (int q = 0; q < P_; ++q) dsp[q] = static_cast<std::int64_t>(q) * per;
+      std::vector<Transfer> xs;
+      append_alltoallv(xs, me_, P_, cnt.data(), dsp.data(), cnt.data(), dsp.data());
       const long long saved = minBytes_;
       minBytes_ = 0;  // every route, whatever the production threshold
-      alltoallv(send, cnt.data(), dsp.data(), recv, cnt.data(), dsp.data(), nullptr);
+      // the registered path the executors use: device barriers, plane stream
+      const int id = register_exchange(0, xs);
       minBytes_ = saved;
+      exchange_registered(id, nullptr, nullptr);
       gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      reg_.pop_back();
       std::vector<unsigned long long> got(pattern.size());
       gpu_check(hipMemcpy(got.data(), recv, got.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy");
       for (int q = 0; q < P_ && ok; ++q)
@@ -1150,97 +1285,211 @@ public:
     if (process_exiting()) return;
     try {
       DeviceGuard guard(device_);
+      // the last registered exchange has finished before its buffers go
+      if (channel_) (void)hipStreamSynchronize(channel_->stream->get());
+      if (evIn_) (void)hipEventDestroy(evIn_);
+      if (evOut_) (void)hipEventDestroy(evOut_);
       for (void* p : opened_) ipc_close(p);
     } catch (...) {
     }
   }
 
+  // Split of every peer message (from every rank's transfer list; `all` holds
+  // W entries per rank, unused ones of kind -1) into the direct part and one
+  // share per relay, and this rank's copy segments: phase 1 (own block; relay
+  // shares into this rank's relay buffers) and phase 2 (direct parts out of the
+  // senders' send sides, relay shares out of the senders' relay buffers). A list
+  // may hold several messages per ordered pair (pipelined steps carry one
+  // all-to-all per plane chunk): the m-th send p -> q pairs with the m-th
+  // receive q <- p (NCCL's matching rule).
+  void build_segs(const char* s, char* r, int sendSlot, const std::vector<Transfer>& xs,
+                  const std::vector<Transfer>& all, int W, std::vector<dev::CopySeg>& push,
+                  std::vector<dev::CopySeg>& pull) const {
+    struct Msg {
+      int p, q;
+      long long so, ro, nb, base, roff;
+    };
+    std::vector<Msg> msgs;
+    std::map<std::tuple<int, int, int>, std::size_t> byKey;  // (p, q, m) -> message
+    std::vector<int> nSend(P_ * P_, 0), nRecv(P_ * P_, 0);
+    for (int p = 0; p < P_; ++p)
+      for (int i = 0; i < W; ++i) {
+        const Transfer& t = all[static_cast<std::size_t>(p) * W + i];
+        if (t.kind != Transfer::kSend || t.peer < 0 || t.peer >= P_) continue;
+        const int m = nSend[p * P_ + t.peer]++;
+        byKey[std::make_tuple(p, t.peer, m)] = msgs.size();
+        msgs.push_back(Msg{p, t.peer, t.offset, -1, t.bytes, 0, 0});
+      }
+    for (int q = 0; q < P_; ++q)
+      for (int i = 0; i < W; ++i) {
+        const Transfer& t = all[static_cast<std::size_t>(q) * W + i];
+        if (t.kind != Transfer::kRecv || t.peer < 0 || t.peer >= P_) continue;
+        const int m = nRecv[t.peer * P_ + q]++;
+        auto it = byKey.find(std::make_tuple(t.peer, q, m));
+        if (it == byKey.end() || msgs[it->second].nb != t.bytes) mismatch();
+        msgs[it->second].ro = t.offset;
+      }
+    if (nSend != nRecv) mismatch();
+    // shares: base per relay (16-byte multiple), the direct part the rest; a
+    // sender's relay buffer holds its shares in message order
+    std::vector<long long> used(P_, 0);
+    for (Msg& g : msgs) {
+      long long b = 0;
+      if (g.q != g.p && K_ > 0 && g.nb >= minBytes_) b = (g.nb / (P_ - 1 + K_)) / 16 * 16;
+      if (used[g.p] + b > capOf_[g.p]) b = 0;  // sender p's relay buffers
+      g.base = b;
+      g.roff = used[g.p];
+      used[g.p] += b;
+    }
+    auto add = [](std::vector<dev::CopySeg>& v, const char* src, char* dst, long long bytes) {
+      if (bytes > 0) v.push_back(dev::CopySeg{src, dst, static_cast<unsigned long long>(bytes), 0});
+    };
+    push.clear();
+    pull.clear();
+    for (const Transfer& t : xs)
+      if (t.kind == Transfer::kLocal) add(push, s + t.offset, r + t.dstOffset, t.bytes);
+    for (const Msg& g : msgs) {
+      if (g.p == g.q || g.nb == 0) continue;
+      const long long direct = g.nb - K_ * g.base;
+      if (g.p == me_)
+        for (int c = 0; c < K_ && g.base > 0; ++c)
+          add(push, s + g.so + direct + c * g.base, peers_[me_][2 + c] + g.roff, g.base);
+      if (g.q == me_) {
+        add(pull, peers_[g.p][sendSlot] + g.so, r + g.ro, direct);
+        for (int c = 0; c < K_ && g.base > 0; ++c)
+          add(pull, peers_[g.p][2 + c] + g.roff, r + g.ro + direct + c * g.base, g.base);
+      }
+    }
+    auto number = [](std::vector<dev::CopySeg>& v) {
+      long long chunks = 0;
+      for (dev::CopySeg& g : v) {
+        g.firstChunk = chunks;
+        chunks += (static_cast<long long>(g.bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
+      }
+    };
+    number(push);
+    number(pull);
+  }
+
+  // every rank's transfer list, padded to the longest (W entries per rank,
+  // returned in *W)
+  std::vector<Transfer> gather_lists(const std::vector<Transfer>& xs, bool host, int* W) {
+    const int mine = static_cast<int>(xs.size());
+    std::vector<int> sizes(P_);
+    if (host)
+      host_allgather(&mine, sizes.data(), sizeof(int));
+    else
+      comm_->allgather(&mine, sizes.data(), sizeof(int));
+    *W = std::max(1, *std::max_element(sizes.begin(), sizes.end()));
+    std::vector<Transfer> wire(*W, Transfer{-1, 0, 0, 0, 0});
+    std::copy(xs.begin(), xs.end(), wire.begin());
+    std::vector<Transfer> all(static_cast<std::size_t>(*W) * P_);
+    if (host)
+      host_allgather(wire.data(), all.data(), sizeof(Transfer) * *W);
+    else
+      comm_->allgather(wire.data(), all.data(), sizeof(Transfer) * *W);
+    return all;
+  }
+
+  int slot_of(const void* p) const { return p == local_buffer(0) ? 0 : (p == local_buffer(1) ? 1 : -1); }
+
+  // Unregistered exchange (host-synchronous): the lists are gathered per call,
+  // the phases are separated by host barriers.
   void exchange(const void* send, void* recv, const std::vector<Transfer>& xs, hipStream_t stream,
                 const ExchangeSync* sync) override {
     SPFFT_TIMED_SCOPE("relay_exchange");
     DeviceGuard guard(device_);
-    const int recvSlot = recv == local_buffer(0) ? 0 : (recv == local_buffer(1) ? 1 : -1);
+    const int recvSlot = slot_of(recv);
     const int sendSlot = 1 - recvSlot;
     // the grid's exchange sides only
     if (recvSlot < 0 || send != local_buffer(sendSlot)) throw InternalError();
+    check();
     sync_begin(sync, stream);
-    // every rank's transfer list (fixed size: own block + one send and one
-    // receive per peer); the host collective overlaps the GPU work still
-    // queued ahead of the exchange (the stream is synchronised before the
-    // barrier that lets peers read this rank's send side)
-    const int W = 2 * P_ + 1;
-    std::vector<Transfer> wire(W, Transfer{-1, 0, 0, 0, 0});
-    if (static_cast<int>(xs.size()) > W) throw InternalError();
-    std::copy(xs.begin(), xs.end(), wire.begin());
-    std::vector<Transfer> all(static_cast<std::size_t>(W) * P_);
-    host_allgather(wire.data(), all.data(), sizeof(Transfer) * W);
-    // matched pairs p -> q: send offset, receive offset, bytes (NCCL matching
-    // rule: one send and one receive per ordered pair in these lists)
-    std::vector<long long> so(P_ * P_, -1), ro(P_ * P_, -1), nb(P_ * P_, 0);
-    for (int p = 0; p < P_; ++p)
-      for (int i = 0; i < W; ++i) {
-        const Transfer& t = all[static_cast<std::size_t>(p) * W + i];
-        if (t.kind == Transfer::kSend) {
-          so[p * P_ + t.peer] = t.offset;
-          nb[p * P_ + t.peer] = t.bytes;
-        } else if (t.kind == Transfer::kRecv) {
-          ro[t.peer * P_ + p] = t.offset;
-        }
-      }
-    // shares: base per relay (16-byte multiple), the direct part the rest
-    std::vector<long long> base(P_ * P_, 0), roff(P_ * P_, 0);
-    for (int p = 0; p < P_; ++p) {
-      long long used = 0;
-      for (int q = 0; q < P_; ++q) {
-        const long long m = nb[p * P_ + q];
-        long long b = 0;
-        if (q != p && K_ > 0 && m >= minBytes_) b = (m / (P_ - 1 + K_)) / 16 * 16;
-        if (used + b > capOf_[p]) b = 0;  // sender p's relay buffers
-        base[p * P_ + q] = b;
-        roff[p * P_ + q] = used;
-        used += b;
-      }
-    }
-    const char* s = static_cast<const char*>(send);
-    char* r = static_cast<char*>(recv);
-    for (int p = 0; p < P_; ++p)
-      for (int q = 0; q < P_; ++q)
-        if (p != q && nb[p * P_ + q] > 0 && (so[p * P_ + q] < 0 || ro[p * P_ + q] < 0)) mismatch();
-    // phase 1: own block, relay pushes
-    segCount_ = 0;
-    for (const Transfer& t : xs)
-      if (t.kind == Transfer::kLocal) add_seg(s + t.offset, r + t.dstOffset, t.bytes);
-    for (int q = 0; q < P_; ++q) {
-      const int k = me_ * P_ + q;
-      if (q == me_ || base[k] == 0) continue;
-      const long long direct = nb[k] - K_ * base[k];
-      for (int c = 0; c < K_; ++c)
-        add_seg(s + so[k] + direct + c * base[k], peers_[me_][2 + c] + roff[k], base[k]);
-    }
-    run_segs(stream);
+    // (the host collective overlaps the GPU work still queued ahead of the
+    // exchange; the stream is synchronised before the barrier that lets peers
+    // read this rank's send side)
+    int W = 0;
+    const std::vector<Transfer> all = gather_lists(xs, true, &W);
+    std::vector<dev::CopySeg> push, pull;
+    build_segs(static_cast<const char*>(send), static_cast<char*>(recv), sendSlot, xs, all, W, push, pull);
+    run_segs(push, stream);
     gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     host_barrier();
-    // phase 2: pull the direct parts and the relayed shares addressed here
-    segCount_ = 0;
-    for (int p = 0; p < P_; ++p) {
-      const int k = p * P_ + me_;
-      if (p == me_ || nb[k] == 0) continue;
-      const long long direct = nb[k] - K_ * base[k];
-      add_seg(peers_[p][sendSlot] + so[k], r + ro[k], direct);
-      for (int c = 0; c < K_ && base[k] > 0; ++c)
-        add_seg(peers_[p][2 + c] + roff[k], r + ro[k] + direct + c * base[k], base[k]);
-    }
-    if (segCount_ > 0) {
-      run_segs(stream);
+    if (!pull.empty()) {
+      run_segs(pull, stream);
       gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
     }
     host_barrier();  // send sides and relay buffers are free again
     sync_end(sync, stream);
   }
+
+  // Registered exchanges (the executors' plans): the split and both segment
+  // tables are computed once, collectively, at plan time and kept on the
+  // device; an exchange is then four launches on the plane's stream and no
+  // host round trip: push, barrier round, pull, barrier round (the senders'
+  // send sides and relay buffers are free again).
+  int register_exchange(int sendSlot, const std::vector<Transfer>& xs) override {
+    DeviceGuard guard(device_);
+    int W = 0;
+    const std::vector<Transfer> all = gather_lists(xs, false, &W);
+    std::vector<dev::CopySeg> push, pull;
+    const char* s = static_cast<const char*>(local_buffer(sendSlot));
+    char* r = static_cast<char*>(local_buffer(1 - sendSlot));
+    if (!xs.empty() && (!s || !r)) throw InternalError();
+    build_segs(s, r, sendSlot, xs, all, W, push, pull);
+    Registered g;
+    auto up = [](std::unique_ptr<DeviceBuffer>& b, const std::vector<dev::CopySeg>& v) {
+      if (v.empty()) return;
+      b.reset(new DeviceBuffer(v.size() * sizeof(dev::CopySeg)));
+      gpu_check(hipMemcpy(b->data(), v.data(), v.size() * sizeof(dev::CopySeg), hipMemcpyHostToDevice), "hipMemcpy");
+    };
+    up(g.push, push);
+    up(g.pull, pull);
+    g.nPush = static_cast<int>(push.size());
+    g.nPull = static_cast<int>(pull.size());
+    g.chPush = push.empty() ? 0 : push.back().firstChunk + (static_cast<long long>(push.back().bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
+    g.chPull = pull.empty() ? 0 : pull.back().firstChunk + (static_cast<long long>(pull.back().bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
+    reg_.push_back(std::move(g));
+    return static_cast<int>(reg_.size()) - 1;
+  }
+
+  void exchange_registered(int id, hipStream_t stream, const ExchangeSync* sync) override {
+    SPFFT_TIMED_SCOPE("relay_exchange");
+    DeviceGuard guard(device_);
+    check();
+    const Registered& g = reg_.at(static_cast<std::size_t>(id));
+    std::lock_guard<std::mutex> lock(channel_->m);
+    hipStream_t cs = channel_->stream->get();
+    if (!sync) {
+      gpu_check(hipEventRecord(evIn_, stream), "hipEventRecord");
+      gpu_check(hipStreamWaitEvent(cs, evIn_, 0), "hipStreamWaitEvent");
+    }
+    sync_begin(sync, cs);
+    if (g.nPush) dev::launch_multi_copy(g.push->data<dev::CopySeg>(), g.nPush, g.chPush, cs);
+    bar_.round(cs);
+    if (g.nPull) dev::launch_multi_copy(g.pull->data<dev::CopySeg>(), g.nPull, g.chPull, cs);
+    bar_.round(cs);
+    sync_end(sync, cs);
+    if (!sync) {
+      gpu_check(hipEventRecord(evOut_, cs), "hipEventRecord");
+      gpu_check(hipStreamWaitEvent(stream, evOut_, 0), "hipStreamWaitEvent");
+    }
+  }
+  hipStream_t channel_stream() const override { return channel_ ? channel_->stream->get() : nullptr; }
+  void check() override {
+    std::string d;
+    if (!bar_.healthy(&d)) {
+      set_error_detail(d);
+      throw MPIError();
+    }
+  }
+  bool healthy(std::string* detail) override { return bar_.healthy(detail); }
+  void abort() override { bar_.abort(); }
+
   int plane_rank() const override { return me_; }
   int plane_size() const override { return P_; }
-  bool host_synchronous() const override { return true; }
-  int max_pipeline_steps() const override { return 1; }
+  bool host_synchronous() const override { return false; }
+  int max_pipeline_steps() const override { return 0; }
   void* local_buffer(int slot) const override {
     if (slot < 0 || slot > 1 || !sides_[slot]) return nullptr;
     return sides_[slot]->data();
@@ -1263,7 +1512,7 @@ public:
 
 private:
   static constexpr int kMaxRelays = 8;
-  [[noreturn]] void mismatch() {
+  [[noreturn]] void mismatch() const {
     set_error_detail("relay exchange: transfer lists of the ranks do not match");
     throw MPIError();
   }
@@ -1274,34 +1523,36 @@ private:
       comm_->barrier();
   }
   void host_allgather(const void* send, void* recv, std::size_t bytes) {
-    if (shm_)
+    if (shm_ && bytes <= shmPayload_)
       shm_->allgather(send, recv, bytes);
     else
       comm_->allgather(send, recv, bytes);
   }
-  void add_seg(const char* src, char* dst, long long bytes) {
-    if (bytes <= 0) return;
-    if (segCount_ >= segsHost_.size()) throw InternalError();
-    segsHost_[segCount_++] = dev::CopySeg{src, dst, static_cast<unsigned long long>(bytes), 0};
-  }
-  void run_segs(hipStream_t stream) {
-    long long chunks = 0;
-    for (std::size_t i = 0; i < segCount_; ++i) {
-      segsHost_[i].firstChunk = chunks;
-      chunks += (static_cast<long long>(segsHost_[i].bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
-    }
-    if (segCount_ == 0) return;
-    if (segCount_ <= static_cast<std::size_t>(dev::kInlineSegs)) {
-      // the table travels in the kernel arguments (no host-to-device copy)
-      std::copy(segsHost_.begin(), segsHost_.begin() + static_cast<std::ptrdiff_t>(segCount_), inlineSegs_.s);
-      dev::launch_multi_copy_inline(inlineSegs_, static_cast<int>(segCount_), chunks, stream);
+  // one host-built segment table: in the kernel arguments when it fits, else
+  // through the staging buffer (host-synchronous path only)
+  void run_segs(const std::vector<dev::CopySeg>& segs, hipStream_t stream) {
+    if (segs.empty()) return;
+    const long long chunks = segs.back().firstChunk +
+                             (static_cast<long long>(segs.back().bytes) + dev::kCopyChunk - 1) / dev::kCopyChunk;
+    if (segs.size() <= static_cast<std::size_t>(dev::kInlineSegs)) {
+      std::copy(segs.begin(), segs.end(), inlineSegs_.s);
+      dev::launch_multi_copy_inline(inlineSegs_, static_cast<int>(segs.size()), chunks, stream);
       return;
     }
-    gpu_check(hipMemcpyAsync(segsDev_->data(), segsHost_.data(), segCount_ * sizeof(dev::CopySeg),
+    if (!segsDev_ || segsDev_->bytes() < segs.size() * sizeof(dev::CopySeg))
+      segsDev_.reset(new DeviceBuffer(segs.size() * sizeof(dev::CopySeg)));
+    gpu_check(hipMemcpyAsync(segsDev_->data(), segs.data(), segs.size() * sizeof(dev::CopySeg),
                              hipMemcpyHostToDevice, stream),
               "hipMemcpyAsync");
-    dev::launch_multi_copy(segsDev_->data<dev::CopySeg>(), static_cast<int>(segCount_), chunks, stream);
+    dev::launch_multi_copy(segsDev_->data<dev::CopySeg>(), static_cast<int>(segs.size()), chunks, stream);
+    gpu_check(hipStreamSynchronize(stream), "hipStreamSynchronize");  // the staging buffer is reused
   }
+
+  struct Registered {
+    std::unique_ptr<DeviceBuffer> push, pull;
+    int nPush = 0, nPull = 0;
+    long long chPush = 0, chPull = 0;
+  };
 
   std::shared_ptr<Communicator> comm_;
   int device_, me_, P_, K_;
@@ -1316,11 +1567,14 @@ private:
   std::vector<std::unique_ptr<IpcLease>> relay_;
   std::vector<std::vector<char*>> peers_;  // [rank][0: stick side, 1: slab side, 2 + c: relay c]
   std::vector<void*> opened_;
-  std::vector<dev::CopySeg> segsHost_;
-  std::size_t segCount_ = 0;
   std::unique_ptr<DeviceBuffer> segsDev_;
   std::unique_ptr<ShmGroup> shm_;
+  std::size_t shmPayload_ = 0;  // largest allgather the shared segment carries
   dev::SegPack inlineSegs_{};
+  std::vector<Registered> reg_;       // registered exchanges (plan time)
+  BarrierRounds bar_;                 // device barrier rounds of the registered path
+  std::shared_ptr<PeerChannel> channel_;  // ordered stream of the registered exchanges
+  hipEvent_t evIn_ = nullptr, evOut_ = nullptr;
 };
 
 struct NodeInfo {
@@ -1333,28 +1587,122 @@ struct NodeInfo {
   int relay;   // SPFFT_RELAY: 0 auto, 1 off, 2 force (virtual relays)
   int relayVirtual;  // SPFFT_RELAY_VIRTUAL
   unsigned long long stickBytes;  // this rank's stick side (per-peer message estimate)
+  int localSize;  // the launcher's ranks on this node (0 unknown)
 };
 
 // SPFFT_RELAY=auto: whether relaying through K idle GPUs beats the direct
-// links for per-peer messages of m bytes among n ranks. Direct: m at one link's
-// rate; relay: two hops of (n - 1) / (n - 1 + K) of m each, plus ~60 us of
-// host round trips (two stream synchronisations, the node-local shared-memory
-// allgather and barriers: 42-53 us per exchange measured with 2 ranks on one
-// MI355X, 220-280 us through the gloo control plane; profiles/r5/relay/
-// overhead.txt). Relay is chosen when it models at least 20% faster: N = 2 at
-// 256^3 fp64 (52 MB per peer, K = 6: 750 vs 275 us) relays; N = 4 (13 MB,
-// K = 4: 190 vs 220 us) and small problems stay on RCCL.
-bool relay_pays(double m, int n, int k) {
-  constexpr double kLinkBytesPerUs = 70e3, kHostUs = 60.0;
-  const double direct = m / kLinkBytesPerUs;
-  const double relay = 2.0 * m * (n - 1) / (n - 1 + k) / kLinkBytesPerUs + kHostUs;
+// links for per-peer messages of m bytes among n ranks, at the measured link
+// rate (measure_link_GBps; 70 GB/s if unknown). Direct: m at one link's rate;
+// relay: two stream-ordered hops (push, pull) of (n - 1) / (n - 1 + K) of m
+// each plus two barrier rounds (~10 us each). Relay is chosen when it models
+// at least 20% faster: N = 2 at 256^3 fp64 (52 MB per peer, K = 6: 750 vs
+// 235 us at 70 GB/s) relays; small problems stay on RCCL.
+bool relay_pays(double m, int n, int k, double linkGBps) {
+  const double bytesPerUs = (linkGBps > 0 ? linkGBps : 70.0) * 1e3;
+  constexpr double kBarrierUs = 20.0;
+  const double direct = m / bytesPerUs;
+  const double relay = 2.0 * m * (n - 1) / (n - 1 + k) / bytesPerUs + kBarrierUs;
   return relay < 0.8 * direct;
+}
+
+double measure_link_GBps(Communicator& comm, int device);
+
+// The link rate of a member set's node (measured once per process and key).
+double node_link_rate(Communicator& comm, int device, const std::string& key) {
+  static std::mutex m;
+  static std::map<std::string, double> cache;
+  {
+    std::lock_guard<std::mutex> lock(m);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  const double r = measure_link_GBps(comm, device);
+  std::lock_guard<std::mutex> lock(m);
+  cache[key] = r;
+  return r;
 }
 
 int env_relay() {
   const char* e = std::getenv("SPFFT_RELAY");
   const std::string v = e ? e : "";
   return v == "0" || v == "off" ? 1 : (v == "force" ? 2 : 0);
+}
+
+// Collective (ranks of one node on distinct GPUs). The usable one-way rate of
+// one xGMI link: every rank copies 8 MiB into its right neighbour's memory (an
+// IPC-mapped arena block), all links of the ring at once, best of 3 timed
+// copies; the median over ranks in GB/s (0 if the probe could not run). It
+// replaces the link-rate assumption of the relay decision and is reported in
+// the plane info (bench.py's model).
+double measure_link_GBps(Communicator& comm, int device) {
+  constexpr std::size_t kBytes = std::size_t(8) << 20;
+  const int P = comm.size(), me = comm.rank();
+  DeviceGuard guard(device);
+  int ok = 1;
+  std::unique_ptr<IpcLease> target;
+  std::unique_ptr<DeviceBuffer> src;
+  IpcExport mine{};
+  try {
+    target = ipc_acquire(device, kBytes, false);
+    src.reset(new DeviceBuffer(kBytes));
+    gpu_check(hipMemset(src->data(), 1, kBytes), "hipMemset");
+    mine = target->describe();
+  } catch (const std::exception&) {
+    ok = 0;
+  }
+  std::vector<IpcExport> all(P);
+  comm.allgather(&mine, all.data(), sizeof(IpcExport));
+  void* dst = nullptr;
+  const int right = (me + 1) % P;
+  if (ok && all[right].valid) {
+    try {
+      std::string why;
+      dst = ipc_open_checked(all[right], &why);
+      const int ndev = [] {
+        int n = 0;
+        return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+      }();
+      for (int d = 0; d < ndev; ++d)
+        if (d != device) (void)hipDeviceEnablePeerAccess(d, 0);
+      (void)hipGetLastError();
+    } catch (const std::exception&) {
+      dst = nullptr;
+    }
+  }
+  double best = 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  comm.barrier();
+  if (dst && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+    GpuStream st(false);
+    for (int it = 0; it < 4; ++it) {
+      (void)hipEventRecord(e0, st.get());
+      (void)hipMemcpyAsync(dst, src->data(), kBytes, hipMemcpyDeviceToDevice, st.get());
+      (void)hipEventRecord(e1, st.get());
+      float ms = 0;
+      if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && it > 0 &&
+          ms > 0)
+        best = std::max(best, kBytes / (ms * 1e-3) / 1e9);
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipGetLastError();
+  comm.barrier();  // every copy into a peer's block is done before the blocks go
+  if (dst) ipc_close(dst);
+  std::vector<double> rates(P);
+  comm.allgather(&best, rates.data(), sizeof(double));
+  std::sort(rates.begin(), rates.end());
+  return rates[P / 2];
+}
+
+// Ranks of this job on this node according to the launcher (torchrun,
+// Open MPI, MPICH/Hydra), 0 if unknown.
+int launcher_local_size() {
+  for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"}) {
+    const char* e = std::getenv(v);
+    if (e && *e) return std::atoi(e);
+  }
+  return 0;
 }
 
 // Collective. The GPUs of this node that no rank of the group runs on and
@@ -1375,12 +1723,18 @@ std::vector<int> idle_devices(Communicator& comm, const std::vector<PciId>& used
   const int P = comm.size();
   std::vector<Visible> all(P);
   comm.allgather(&mine, all.data(), sizeof(Visible));
-  // candidates: rank 0's devices no rank uses
+  // candidates: rank 0's devices no rank uses and nothing else uses either
+  // (rank 0 decides from the driver's counters; the list is agreed below)
   std::vector<PciId> cand;
+  std::vector<int> idle(all[0].n, 0);
+  if (comm.rank() == 0)
+    for (int d = 0; d < all[0].n; ++d) idle[d] = relay_candidate_idle(all[0].id[d].domain, all[0].id[d].bus, all[0].id[d].device) ? 1 : 0;
+  std::vector<int> idleAll(static_cast<std::size_t>(all[0].n) * P);
+  if (all[0].n > 0) comm.allgather(idle.data(), idleAll.data(), sizeof(int) * all[0].n);
   for (int d = 0; d < all[0].n; ++d) {
     bool inUse = false;
     for (const PciId& u : used) inUse = inUse || u == all[0].id[d];
-    if (!inUse && static_cast<int>(cand.size()) < kMaxRelay) cand.push_back(all[0].id[d]);
+    if (!inUse && idleAll[d] && static_cast<int>(cand.size()) < kMaxRelay) cand.push_back(all[0].id[d]);
   }
   // keep those every rank sees; this process's ordinal of each
   std::vector<int> out;
@@ -1457,7 +1811,46 @@ std::shared_ptr<NcclChannel> acquire_channel(Communicator* group, const std::str
 
 }  // namespace
 
+// Bytes of device memory in use on the GPU at a PCI location, from the amdgpu
+// driver's sysfs (no HIP context on that GPU); -1 if unknown. SPFFT_SYSFS_ROOT
+// (tests) replaces /sys.
+long long vram_used_bytes_at(int domain, int bus, int device) {
+  const char* root = std::getenv("SPFFT_SYSFS_ROOT");
+  char path[256];
+  std::snprintf(path, sizeof(path), "%s/bus/pci/devices/%04x:%02x:%02x.0/mem_info_vram_used",
+                root && *root ? root : "/sys", domain & 0xffff, bus & 0xff, device & 0xff);
+  std::FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  long long v = -1;
+  if (std::fscanf(f, "%lld", &v) != 1) v = -1;
+  std::fclose(f);
+  return v;
+}
+
+// A relay candidate must be idle: no process holds more than the driver's own
+// few MiB of its memory (another job, or another communicator of this job,
+// would otherwise get this job's buffers and link traffic). Unknown usage
+// counts as busy.
+constexpr long long kIdleVramBytes = 256ll << 20;
+bool relay_candidate_idle(int domain, int bus, int device) {
+  const long long used = vram_used_bytes_at(domain, bus, device);
+  return used >= 0 && used <= kIdleVramBytes;
+}
+
 int DeviceComm::rccl_channels_created() { return gChannelsCreated.load(); }
+
+void DeviceComm::exchange_registered(int, hipStream_t, const ExchangeSync*) { throw InternalError(); }
+
+std::string DeviceComm::info() const {
+  std::string j = info_json();
+  if (linkGBps_ > 0 && !j.empty() && j.back() == '}') {
+    char b[64];
+    std::snprintf(b, sizeof(b), ", \"link_GBps_measured\": %.1f}", linkGBps_);
+    j.pop_back();
+    j += b;
+  }
+  return j;
+}
 
 std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicator>& comm,
                                                int device, SpfftExchangeType exchange,
@@ -1519,6 +1912,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   mine.fault = env_fault();
   mine.relay = env_relay();
   mine.stickBytes = bytes[0];
+  mine.localSize = launcher_local_size();
   {
     const char* rv = std::getenv("SPFFT_RELAY_VIRTUAL");
     mine.relayVirtual = rv && *rv ? std::max(1, std::min(8, std::atoi(rv))) : 2;
@@ -1545,8 +1939,19 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   // exchanges of ranks on distinct GPUs when other GPUs are idle (SPFFT_RELAY
   // auto), or through virtual relays on the ranks' own GPUs (force, tests)
   const int relayMode = all[0].relay;
+  // ranks of one node on distinct GPUs: the link rate, measured (setup cost a
+  // few ms, once per member set)
+  const double linkGBps = oneNode && !sharedDevice && P > 1 ? node_link_rate(*comm, device, key) : 0.0;
+  auto finish = [&](std::unique_ptr<DeviceComm> dc) {
+    dc->set_link_rate(linkGBps);
+    return dc;
+  };
+  // auto relay only when this group is every rank of the job on the node (the
+  // launcher's local size): GPUs that no rank of this group uses may belong
+  // to another communicator of the job
+  const int localSize = all[0].localSize;
   if (oneNode && !unbuffered && fault == 0 && prefer == 0 && relayMode != 1 &&
-      (relayMode == 2 || !sharedDevice)) {
+      (relayMode == 2 || (!sharedDevice && (localSize == 0 || localSize == P)))) {
     std::vector<int> relays;
     if (relayMode == 2) {
       relays.assign(all[0].relayVirtual, device);
@@ -1557,10 +1962,10 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     }
     double perPeer = 0;
     for (int q = 0; q < P; ++q) perPeer = std::max(perPeer, static_cast<double>(all[q].stickBytes) / P);
-    const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()));
+    const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()), linkGBps);
     if (!relays.empty() && pays) {
       try {
-        return std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays));
+        return finish(std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays, "relay" + key)));
       } catch (const MPIError&) {
         // every rank agreed on the failure (setup or self-test): the next plane
         if (comm->rank() == 0)
@@ -1572,7 +1977,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
   if (peer) {
     try {
-      return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
+      return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key)));
     } catch (const PeerSelfTestFailed&) {
       // every rank saw the failure: ranks on distinct devices move the data
       // through RCCL instead (UNBUFFERED included); ranks sharing a device
@@ -1588,7 +1993,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   comm->allgather(&ok, oks.data(), sizeof(int));
   bool allOk = true;
   for (int v : oks) allOk = allOk && v != 0;
-  if (allOk) return std::unique_ptr<DeviceComm>(new RcclDeviceComm(ch));
+  if (allOk) return finish(std::unique_ptr<DeviceComm>(new RcclDeviceComm(ch)));
   const std::string why = ch->ok() ? std::string("RCCL: another rank failed to initialise") : ch->detail;
   ch->abort();
   ch.reset();
@@ -1600,7 +2005,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   }
   if (comm->rank() == 0)
     std::fprintf(stderr, "spfft: %s; using the peer-write (IPC) data plane\n", why.c_str());
-  return std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key));
+  return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key)));
 }
 
 }  // namespace spfft

@@ -75,6 +75,12 @@ struct ExchangeSync {
   hipEvent_t end;
 };
 
+// Whether an idle-GPU relay candidate (PCI location) is idle: the amdgpu
+// driver reports at most a few MiB of its memory in use (sysfs
+// mem_info_vram_used; SPFFT_SYSFS_ROOT replaces /sys in tests). Unknown usage
+// counts as busy. The relay plane never leases memory on a busy GPU.
+bool relay_candidate_idle(int domain, int bus, int device);
+
 class DeviceComm {
 public:
   // Collective. `buffers` are the grid's two exchange slots (0 = stick side,
@@ -90,6 +96,14 @@ public:
   // without a stream of their own run it on `stream`.
   virtual void exchange(const void* send, void* recv, const std::vector<Transfer>& xs,
                         hipStream_t stream, const ExchangeSync* sync) = 0;
+  // Collective for planes that precompute their exchanges (the relay plane):
+  // every rank registers its transfer list of one exchange (sent from its side
+  // `sendSlot`, received into the other side) in the same order, at plan time.
+  // Returns the id for exchange_registered, or -1 (the plane does not
+  // register; then the call is not collective and exchange() is used).
+  virtual int register_exchange(int /*sendSlot*/, const std::vector<Transfer>& /*xs*/) { return -1; }
+  // Runs a registered exchange, stream-ordered (sync as for exchange()).
+  virtual void exchange_registered(int id, hipStream_t stream, const ExchangeSync* sync);
   // Byte counts / displacements, one entry per rank, as one exchange().
   void alltoallv(const void* send, const std::int64_t* sendCounts, const std::int64_t* sendDispls,
                  void* recv, const std::int64_t* recvCounts, const std::int64_t* recvDispls,
@@ -146,8 +160,15 @@ public:
   // bus ids of every GPU the plane touches: the ranks' and any relay GPUs),
   // "link_GBps_measured" (copy probe at setup). Stable for the plane's life.
   virtual std::string info_json() const { return std::string("{\"kind\": \"") + kind() + "\"}"; }
+  // info_json() plus "link_GBps_measured" when the link probe ran
+  std::string info() const;
+  void set_link_rate(double gbps) { linkGBps_ = gbps; }
+  double link_rate() const { return linkGBps_; }
   // RCCL communicators this process has created (shared channels count once).
   static int rccl_channels_created();
+
+private:
+  double linkGBps_ = 0;  // measured link rate (ranks of one node on distinct GPUs), 0 if none
 };
 
 }  // namespace spfft

@@ -158,8 +158,31 @@ GpuExecutor<T>::GpuExecutor(std::shared_ptr<GridImpl<T>> grid,
     blocks = all[2];
     for (int r = 0; r < p.size; ++r) chunks = std::min(chunks, all[3 * r + 1]);
     if (chunks * blocks > 1 && !build_chunk_plan(chunks, blocks)) throw InternalError();
+    if (!peerWrites_) register_exchanges();
   }
   log_plan();
+}
+
+// Planes that precompute (the relay plane) get every exchange of the plan
+// once, here, in the same order on every rank; they then run each one without
+// host round trips. Other planes return -1 and nothing is registered.
+template <typename T>
+void GpuExecutor<T>::register_exchanges() {
+  DeviceComm& dc = grid_->device_comm();
+  const IndexPlan& p = *plan_;
+  if (pipelined()) {
+    for (ExchangeStep& st : bwdSteps_) st.id = dc.register_exchange(GridImpl<T>::kStickSide, st.xs);
+    for (ExchangeStep& st : fwdSteps_) st.id = dc.register_exchange(GridImpl<T>::kSlabSide, st.xs);
+    return;
+  }
+  std::vector<Transfer> xs;
+  append_alltoallv(xs, p.rank, p.size, bwdSendCounts_.data(), bwdSendDispls_.data(), bwdRecvCounts_.data(),
+                   bwdRecvDispls_.data());
+  bwdId_ = dc.register_exchange(GridImpl<T>::kStickSide, xs);
+  xs.clear();
+  append_alltoallv(xs, p.rank, p.size, bwdRecvCounts_.data(), bwdRecvDispls_.data(), bwdSendCounts_.data(),
+                   bwdSendDispls_.data());
+  fwdId_ = dc.register_exchange(GridImpl<T>::kSlabSide, xs);
 }
 
 // SPFFT_LOG=1: one line per transform with the plan decisions (engines, layout,
@@ -440,7 +463,9 @@ void GpuExecutor<T>::run_steps(const std::vector<ExchangeStep>& steps, bool back
     const ExchangeSync sync{step_event(st.readyKind, st.readyIdx), step_event(st.doneKind, st.doneIdx),
                             j == 0 && b ? b->get() : nullptr,
                             j + 1 == steps.size() && e ? e->get() : nullptr};
-    if (backward)
+    if (st.id >= 0)
+      dc.exchange_registered(st.id, stream_, &sync);
+    else if (backward)
       dc.exchange(stick, slab, st.xs, stream_, &sync);
     else
       dc.exchange(slab, stick, st.xs, stream_, &sync);
@@ -944,7 +969,10 @@ void GpuExecutor<T>::exchange(bool backward) {
   void* stick = grid_->device_slot(GridImpl<T>::kStickSide);
   void* slab = grid_->device_slot(GridImpl<T>::kSlabSide);
   DeviceComm& dc = grid_->device_comm();
-  if (backward)
+  const int id = backward ? bwdId_ : fwdId_;
+  if (id >= 0)
+    dc.exchange_registered(id, stream_, nullptr);
+  else if (backward)
     dc.alltoallv(stick, bwdSendCounts_.data(), bwdSendDispls_.data(), slab, bwdRecvCounts_.data(),
                  bwdRecvDispls_.data(), stream_);
   else

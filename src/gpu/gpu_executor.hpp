@@ -199,7 +199,11 @@ private:
     std::vector<Transfer> xs;  // transfer list of the step (backward direction)
     int readyKind, readyIdx;   // event the step waits for: 0 none, 1 zEv_[i], 2 chunkEv_[k]
     int doneKind, doneIdx;     // event recorded after it: 0 none, 2 chunkEv_[k], 3 blockEv_[i]
+    int id = -1;               // registered with the data plane (DeviceComm::register_exchange)
   };
+  // registers every exchange of the plan with the data plane (collective)
+  void register_exchanges();
+  int bwdId_ = -1, fwdId_ = -1;  // registered unpipelined exchanges
   int exchChunks_ = 1;   // K
   int stickBlocks_ = 1;  // I
   bool pipelined() const { return exchChunks_ > 1 || stickBlocks_ > 1; }

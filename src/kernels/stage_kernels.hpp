@@ -769,6 +769,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   SPFFT_BATCH_SELECT(a, values, out);
+  const bool ntv = a.ntValues != 0;
   const int B = eng.lines();
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
@@ -819,6 +820,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const bool in0 = j0 < static_cast<unsigned>(len0);
       const bool in1 = j1 < static_cast<unsigned>(len1);
       const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
+      if (ntv) return (in0 || in1) ? ld_stream(&vals[j]) : czero<T>();
       return (in0 || in1) ? ld_values(&vals[j]) : czero<T>();
     }, store);
   }

@@ -10,6 +10,7 @@
 #include "api/c_guard.hpp"
 #include "comm/shm_group.hpp"
 #include "core/fault.hpp"
+#include "gpu/device_comm.hpp"
 
 using namespace spfft;
 
@@ -55,5 +56,9 @@ SpfftError spfft_amd_test_comm_shm_check(SpfftAmdComm comm, int iters, double* s
 }
 
 int spfft_amd_test_fault_injection(void) { return 1; }
+
+int spfft_amd_test_relay_candidate_idle(int domain, int bus, int device) {
+  return relay_candidate_idle(domain, bus, device) ? 1 : 0;
+}
 
 }  // extern "C"

@@ -18,6 +18,8 @@ SPFFT_EXPORT SpfftError spfft_amd_test_comm_shm_check(SpfftAmdComm comm, int ite
                                                       double* commUs);
 /* 1: this library reads the SPFFT_FAULT_* switches (core/fault.hpp). */
 SPFFT_EXPORT int spfft_amd_test_fault_injection(void);
+/* 1 if the relay plane would use the GPU at this PCI location as an idle relay. */
+SPFFT_EXPORT int spfft_amd_test_relay_candidate_idle(int domain, int bus, int device);
 
 #ifdef __cplusplus
 }

@@ -270,12 +270,19 @@ def test_bench_model_relay_shares():
     direct = b._model(stages, 52.7e6, 2, 1, 1)
     relay = b._model(stages, 52.7e6, 2, 1, 1, relays=6)
     assert abs(direct["backward"]["link_ms"] - 52.7e6 / 70e9 * 1e3) < 1e-9
-    assert abs(relay["backward"]["link_ms"] - 2 * direct["backward"]["link_ms"] / 7 - b.RELAY_HOST_MS) < 1e-9
+    assert abs(relay["backward"]["link_ms"] - 2 * direct["backward"]["link_ms"] / 7 - b.RELAY_BARRIER_MS) < 1e-9
     assert direct["backward"]["bound"] == "link" and relay["relay_gpus"] == 6
     assert abs(direct["backward"]["compute_ms"] - 0.25) < 1e-12
     # pipelined grid: all but one step's compute hidden behind the link
     piped = b._model(stages, 52.7e6, 2, 2, 2)
     assert abs(piped["backward"]["predicted_ms"] - (direct["backward"]["link_ms"] + 0.25 / 4)) < 1e-9
+    # a measured link rate replaces the assumption
+    meas = b._model(stages, 52.7e6, 2, 1, 1, link_gbps=50.0)
+    assert meas["link_GBps_source"] == "measured"
+    assert abs(meas["backward"]["link_ms"] - 52.7e6 / 50e9 * 1e3) < 1e-9
+    # the pipelined relay: shares, two hops, overlap
+    rp = b._model(stages, 52.7e6, 2, 4, 2, relays=6)
+    assert abs(rp["forward"]["predicted_ms"] - (max(rp["forward"]["link_ms"], 0.23) + 0.23 / 8)) < 1e-9
 
 
 def test_release_library_has_no_test_hooks():

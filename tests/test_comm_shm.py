@@ -79,3 +79,22 @@ def test_shm_peer_exit_detected():
     r = subprocess.run(cmd, cwd=REPO, env=e, capture_output=True, text=True, timeout=120)
     out = r.stdout + r.stderr
     assert "SHM ERROR rank=0" in out and "has exited" in out, out[-4000:]
+
+
+def test_relay_skips_busy_gpus(tmp_path):
+    """Idle-GPU relaying leases memory only on GPUs nothing else uses: the driver's
+    mem_info_vram_used (sysfs, faked here) must show at most a few MiB; a GPU another
+    process holds memory on, or whose usage is unknown, is not a relay candidate."""
+    for pci, used in (("0000:05:00.0", 12 << 20), ("0000:26:00.0", 4 << 30)):
+        d = tmp_path / "bus" / "pci" / "devices" / pci
+        d.mkdir(parents=True)
+        (d / "mem_info_vram_used").write_text(f"{used}\n")
+    code = ("import ctypes\n"
+            "from spfft_amd.ops._lib import lib\n"
+            "f = lib().spfft_amd_test_relay_candidate_idle\n"
+            "f.argtypes = [ctypes.c_int] * 3\n"
+            "print('IDLE', f(0, 0x05, 0), f(0, 0x26, 0), f(0, 0x45, 0))\n")
+    e = dict(os.environ, SPFFT_SYSFS_ROOT=str(tmp_path), **TESTING_ENV)
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=e, capture_output=True, text=True,
+                       timeout=120)
+    assert "IDLE 1 0 0" in r.stdout, (r.stdout + r.stderr)[-4000:]

@@ -339,6 +339,19 @@ def test_fuzz_dist_relay_forced(gpu):
 
 
 @pytest.mark.gpu
+def test_fuzz_dist_relay_pipelined(gpu):
+    """The relay plane's registered, stream-ordered exchanges (device barrier rounds
+    on the plane's ordered stream, no host round trip) with pipelined plans: 2 plane
+    chunks x 2 stick blocks per direction, random distributions with empty ranks."""
+    code, out = _launch_tool(3, "fuzz_dist.py", "--cases", "24", "--seed", "31",
+                             env_extra={"SPFFT_RELAY": "force", "SPFFT_RELAY_MIN_BYTES": "0",
+                                        "SPFFT_RELAY_VIRTUAL": "2", "SPFFT_EXCH_CHUNKS": "2",
+                                        "SPFFT_EXCH_STICK_BLOCKS": "2"})
+    assert code == 0, out[-4000:]
+    assert "24/24 passed" in out and "plane=relay" in out, out[-4000:]
+
+
+@pytest.mark.gpu
 def test_bench_relay_model(gpu, monkeypatch):
     """bench.py over the forced relay plane: checked round trip on both ranks, and the
     modelled link time accounts for the relay shares."""
