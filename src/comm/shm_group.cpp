@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "core/common.hpp"
+#include "core/fault.hpp"
 #include "spfft/exceptions.hpp"
 
 namespace spfft {
@@ -27,6 +28,17 @@ constexpr std::size_t kHeader = 64;
 std::size_t round_up(std::size_t v, std::size_t a) { return (v + a - 1) / a * a; }
 
 bool process_alive(long long pid) { return pid <= 0 || ::kill(static_cast<pid_t>(pid), 0) == 0 || errno != ESRCH; }
+
+// Identity of this process's pid namespace (the /proc/self/ns/pid link,
+// e.g. "pid:[4026531836]"), hashed; 0 if unreadable.
+unsigned long long pid_namespace_id() {
+  char buf[128] = {0};
+  const ssize_t n = ::readlink("/proc/self/ns/pid", buf, sizeof(buf) - 1);
+  if (n <= 0) return 0;
+  unsigned long long h = 1469598103934665603ull;
+  for (ssize_t i = 0; i < n; ++i) h = (h ^ static_cast<unsigned char>(buf[i])) * 1099511628211ull;
+  return h;
+}
 }  // namespace
 
 ShmGroup::Slot* ShmGroup::slot(int q) const {
@@ -91,6 +103,27 @@ std::unique_ptr<ShmGroup> ShmGroup::create(Communicator& comm, std::size_t maxPa
   if (!all) return nullptr;  // the destructor unmaps
   g->slot(g->me_)->pid.store(static_cast<long long>(getpid()), std::memory_order_relaxed);
   comm.barrier();  // every pid is published before the first wait
+  // The waits detect a peer's exit by its pid, which only means something if
+  // every rank sees every other rank's pid: ranks that share /dev/shm from
+  // different pid namespaces (containers with a shared IPC namespace) would
+  // see a peer's pid as absent, or as an unrelated process. Every rank checks
+  // the namespaces and the published pids; if any check fails anywhere, the
+  // group is not used (the caller falls back to the communicator).
+  struct Check {
+    unsigned long long ns;
+    int pidsOk;
+  };
+  Check c{pid_namespace_id(), 1};
+  // fault injection SHM_PIDNS (testing library): the last rank reports another namespace
+  if (SPFFT_FAULT(SHM_PIDNS) == 1 && g->me_ == g->P_ - 1) c.ns ^= 1;
+  for (int q = 0; q < g->P_; ++q) {
+    const long long pid = g->slot(q)->pid.load(std::memory_order_relaxed);
+    if (pid <= 0 || !process_alive(pid)) c.pidsOk = 0;
+  }
+  std::vector<Check> checks(g->P_);
+  comm.allgather(&c, checks.data(), sizeof(Check));
+  for (const Check& k : checks)
+    if (!k.pidsOk || k.ns != checks[0].ns) return nullptr;
   return g;
 }
 

@@ -22,8 +22,9 @@ namespace spfft {
 class ShmGroup {
 public:
   // Collective over `comm`. nullptr on every rank if any rank could not map the
-  // segment (e.g. ranks in different containers of one host) or if
-  // SPFFT_SHM_COLLECTIVES=0. Waits give up after `timeoutSeconds` (0: never)
+  // segment (e.g. ranks in different containers of one host), if the ranks do
+  // not share one pid namespace or cannot see each other's pids (the exit
+  // detection below needs them), or if SPFFT_SHM_COLLECTIVES=0. Waits give up after `timeoutSeconds` (0: never)
   // and as soon as a waited-for process has exited, with MPIError.
   static std::unique_ptr<ShmGroup> create(Communicator& comm, std::size_t maxPayload, double timeoutSeconds);
   ~ShmGroup();

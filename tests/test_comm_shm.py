@@ -98,3 +98,12 @@ def test_relay_skips_busy_gpus(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=e, capture_output=True, text=True,
                        timeout=120)
     assert "IDLE 1 0 0" in r.stdout, (r.stdout + r.stderr)[-4000:]
+
+
+def test_shm_group_needs_one_pid_namespace():
+    """Ranks that share /dev/shm from different pid namespaces cannot use the pid
+    liveness check of the shared-memory waits: the group is not created on any rank
+    (fault injection SHM_PIDNS: the last rank reports another namespace), and the
+    plane falls back to the communicator's collectives."""
+    for d in _probe(2, {"SPFFT_FAULT_SHM_PIDNS": "1"}):
+        assert d["shm_us"] is None and d["comm_us"] > 0, d
