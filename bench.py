@@ -161,7 +161,7 @@ def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, war
               "relay": {"SPFFT_GPU_EXCHANGE": "", "SPFFT_RELAY": "force" if shared else "auto"}}
     out = {}
     for name, env in planes.items():
-        if name == "rccl" and shared:
+        if name == "rccl" and shared and os.environ.get("SPFFT_RCCL_VIRTUAL_HOSTS") != "1":
             out[name] = {"skipped": "ranks share a GPU (RCCL refuses duplicate devices)"}
             continue
         saved = {k: os.environ.get(k) for k in env}
@@ -404,8 +404,9 @@ def main():
     model = None
     if world > 1 and stages:
         chunks, blocks, peer_writes, relays = t.exchange_plan()
-        model = _model(stages, xstats["max_bytes_sent_per_rank"], world, chunks, blocks, relays,
-                       plane_info.get("link_GBps_measured"))
+        # (a same-device copy rate is no link rate: the model keeps its assumption)
+        link = plane_info.get("link_GBps_measured") if plane_info.get("link_kind") == "xgmi" else None
+        model = _model(stages, xstats["max_bytes_sent_per_rank"], world, chunks, blocks, relays, link)
         model["peer_writes"] = peer_writes
         model["shared_device"] = n_devices < world
     planes_ms = None

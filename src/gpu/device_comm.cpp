@@ -1844,8 +1844,9 @@ void DeviceComm::exchange_registered(int, hipStream_t, const ExchangeSync*) { th
 std::string DeviceComm::info() const {
   std::string j = info_json();
   if (linkGBps_ > 0 && !j.empty() && j.back() == '}') {
-    char b[64];
-    std::snprintf(b, sizeof(b), ", \"link_GBps_measured\": %.1f}", linkGBps_);
+    char b[96];
+    std::snprintf(b, sizeof(b), ", \"link_GBps_measured\": %.1f, \"link_kind\": \"%s\"}", linkGBps_,
+                  linkKind_);
     j.pop_back();
     j += b;
   }
@@ -1939,11 +1940,12 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   // exchanges of ranks on distinct GPUs when other GPUs are idle (SPFFT_RELAY
   // auto), or through virtual relays on the ranks' own GPUs (force, tests)
   const int relayMode = all[0].relay;
-  // ranks of one node on distinct GPUs: the link rate, measured (setup cost a
-  // few ms, once per member set)
-  const double linkGBps = oneNode && !sharedDevice && P > 1 ? node_link_rate(*comm, device, key) : 0.0;
+  // ranks of one node: the peer copy rate, measured (setup cost a few ms,
+  // once per member set); an xGMI link between distinct GPUs, the GPU's own
+  // memory when ranks share one (rehearsals; not used for plane decisions)
+  const double linkGBps = oneNode && P > 1 ? node_link_rate(*comm, device, key) : 0.0;
   auto finish = [&](std::unique_ptr<DeviceComm> dc) {
-    dc->set_link_rate(linkGBps);
+    dc->set_link_rate(linkGBps, sharedDevice ? "same-device" : "xgmi");
     return dc;
   };
   // auto relay only when this group is every rank of the job on the node (the
@@ -1962,7 +1964,8 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
     }
     double perPeer = 0;
     for (int q = 0; q < P; ++q) perPeer = std::max(perPeer, static_cast<double>(all[q].stickBytes) / P);
-    const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()), linkGBps);
+    const bool pays = relayMode == 2 || relay_pays(perPeer, P, static_cast<int>(relays.size()),
+                                                   sharedDevice ? 0.0 : linkGBps);
     if (!relays.empty() && pays) {
       try {
         return finish(std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays, "relay" + key)));

@@ -162,13 +162,17 @@ public:
   virtual std::string info_json() const { return std::string("{\"kind\": \"") + kind() + "\"}"; }
   // info_json() plus "link_GBps_measured" when the link probe ran
   std::string info() const;
-  void set_link_rate(double gbps) { linkGBps_ = gbps; }
+  void set_link_rate(double gbps, const char* kind) {
+    linkGBps_ = gbps;
+    linkKind_ = kind;
+  }
   double link_rate() const { return linkGBps_; }
   // RCCL communicators this process has created (shared channels count once).
   static int rccl_channels_created();
 
 private:
-  double linkGBps_ = 0;  // measured link rate (ranks of one node on distinct GPUs), 0 if none
+  double linkGBps_ = 0;  // measured peer copy rate (ranks of one node), 0 if none
+  const char* linkKind_ = "xgmi";  // "xgmi" (distinct GPUs) or "same-device"
 };
 
 }  // namespace spfft
