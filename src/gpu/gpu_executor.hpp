@@ -204,6 +204,7 @@ private:
   // registers every exchange of the plan with the data plane (collective)
   void register_exchanges();
   int bwdId_ = -1, fwdId_ = -1;  // registered unpipelined exchanges
+  int plainHandoff_ = 0;         // backward stick hand-off through the Infinity Cache
   int exchChunks_ = 1;   // K
   int stickBlocks_ = 1;  // I
   bool pipelined() const { return exchChunks_ > 1 || stickBlocks_ > 1; }

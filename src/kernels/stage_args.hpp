@@ -52,6 +52,7 @@ struct ZArgs {
   // us plain vs 79 us nt at 256^3 fp64 T = 1; batched 75.6 plain vs 59-70 us
   // nt per transform; profiles/r6/zb, zb2)
   int ntValues;
+  int plainSticks;  // backward: stick stores with the default cache policy (see GpuExecutor)
   BatchPtrs batch;
 };
 
@@ -87,6 +88,7 @@ struct YArgs {
   // optional per-column run descriptors (all columns qualify) and their stride
   const ColDesc* colDesc;
   long long colStride;
+  int plainSticks;  // backward: stick loads with the default cache policy (see GpuExecutor)
   BatchPtrs batch;
 };
 

@@ -31,6 +31,21 @@ __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
   w.y = v.y;
   __builtin_nontemporal_store(w, reinterpret_cast<V*>(p));
 }
+// Stick-side accesses of the backward z -> y hand-off: streaming (nt), or with
+// the default cache policy (plain: the lines stay in the 256 MB Infinity
+// Cache, where the y stage finds them) when `plain` is set (GpuExecutor).
+template <typename T>
+__device__ __forceinline__ cx<T> ld_stick(const cx<T>* p, int plain) {
+  if (plain) return *p;
+  return ld_stream(p);
+}
+template <typename T>
+__device__ __forceinline__ void st_stick(cx<T>* p, cx<T> v, int plain) {
+  if (plain)
+    *p = v;
+  else
+    st_stream(p, v);
+}
 // The [z][column][y] intermediate is streamed like the rest.
 template <typename T>
 __device__ __forceinline__ cx<T> ld_inter(const cx<T>* p) {
@@ -776,7 +791,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   const int nl = min(B, a.numSticks - s0);
   const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   auto store = [&](int b, int pos, cx<T> v) {
-    if (b < nl) st_stream(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v));
+    if (b < nl) st_stick(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v), a.plainSticks);
   };
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -866,11 +881,11 @@ __global__ void __launch_bounds__(Eng::kBlock)
       // element a constant offset from it; no segment-mode branch and no 64-bit
       // multiply per element (the other modes below read a table per position)
       const BT* row = in + static_cast<long long>(ls) * seg.stride + Eng::F::lane_pos();
-      eng.global_to_global(lds, tw, [&](int, int, int off) -> cx<T> { return cvt<T>(ld_stream(&row[off])); },
+      eng.global_to_global(lds, tw, [&](int, int, int off) -> cx<T> { return cvt<T>(ld_stick(&row[off], a.plainSticks)); },
                            store);
     } else {
       eng.global_to_global(lds, tw, [&](int, int pos) -> cx<T> {
-        return cvt<T>(ld_stream(&in[seg.at(ls, pos)]));
+        return cvt<T>(ld_stick(&in[seg.at(ls, pos)], a.plainSticks));
       }, store);
     }
   } else {
@@ -1058,7 +1073,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
       // zero source instead: fp32 512^3 R2C y backward 228 -> 212 us, 256^3 neutral;
       // profiles/r5/ab/ymask)
       cx<T> v = czero<T>();
-      if (base != kNoBase && b < zl) v = cvt<T>(ld_stream(in + (base + z0 + b)));
+      if (base != kNoBase && b < zl) v = cvt<T>(ld_stick(in + (base + z0 + b), a.plainSticks));
       return v;
     } else {
       long long base;
@@ -1134,7 +1149,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     stage_rows(eng, lds, zl, n, rows);
     eng.lds_to_global(lds, tw, [&](int b, int, cx<T> v) {
       const long long base = bases[slot++];
-      if (base != kNoBase && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
+      if (base != kNoBase && b < zl) st_stick(&out[base + z0 + b], cvt<typename BT::value_type>(v), a.plainSticks);
     });
     return;
   }

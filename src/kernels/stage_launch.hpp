@@ -12,6 +12,7 @@
 namespace spfft {
 namespace dev {
 
+
 template <typename T, typename BT>
 void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>* tw,
                        hipStream_t stream) {
