@@ -1827,11 +1827,13 @@ long long vram_used_bytes_at(int domain, int bus, int device) {
   return v;
 }
 
-// A relay candidate must be idle: no process holds more than the driver's own
-// few MiB of its memory (another job, or another communicator of this job,
+// A relay candidate must be idle: nothing holds memory on it beyond the
+// driver's own reservation (another job, or another communicator of this job,
 // would otherwise get this job's buffers and link traffic). Unknown usage
-// counts as busy.
-constexpr long long kIdleVramBytes = 256ll << 20;
+// counts as busy. Measured on the MI355X hosts of the round-6 pool: idle GPUs
+// report 284 MiB (297766912 B) in use, GPUs with a torch process 1.5 GB and
+// more (profiles/r6/relay/vram_used.txt).
+constexpr long long kIdleVramBytes = 512ll << 20;
 bool relay_candidate_idle(int domain, int bus, int device) {
   const long long used = vram_used_bytes_at(domain, bus, device);
   return used >= 0 && used <= kIdleVramBytes;

@@ -76,9 +76,10 @@ struct ExchangeSync {
 };
 
 // Whether an idle-GPU relay candidate (PCI location) is idle: the amdgpu
-// driver reports at most a few MiB of its memory in use (sysfs
-// mem_info_vram_used; SPFFT_SYSFS_ROOT replaces /sys in tests). Unknown usage
-// counts as busy. The relay plane never leases memory on a busy GPU.
+// driver reports at most 512 MiB of its memory in use (sysfs
+// mem_info_vram_used, its own reservation is ~284 MiB on MI355X;
+// SPFFT_SYSFS_ROOT replaces /sys in tests). Unknown usage counts as busy. The
+// relay plane never leases memory on a busy GPU.
 bool relay_candidate_idle(int domain, int bus, int device);
 
 class DeviceComm {

@@ -85,7 +85,8 @@ def test_relay_skips_busy_gpus(tmp_path):
     """Idle-GPU relaying leases memory only on GPUs nothing else uses: the driver's
     mem_info_vram_used (sysfs, faked here) must show at most a few MiB; a GPU another
     process holds memory on, or whose usage is unknown, is not a relay candidate."""
-    for pci, used in (("0000:05:00.0", 12 << 20), ("0000:26:00.0", 4 << 30)):
+    # (an idle MI355X reports 297766912 B: the driver's reservation)
+    for pci, used in (("0000:05:00.0", 297766912), ("0000:26:00.0", 1545904128)):
         d = tmp_path / "bus" / "pci" / "devices" / pci
         d.mkdir(parents=True)
         (d / "mem_info_vram_used").write_text(f"{used}\n")
