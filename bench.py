@@ -16,8 +16,12 @@ all-to-all and kernel tails overlap the others' kernels. transforms/sec =
 
 Multi-GPU: launched by torch.distributed.run, one rank per GPU; z-sticks and
 xy-planes are split evenly over ranks and the pencil <-> slab redistribution
-runs as RCCL all-to-all(v) over xGMI inside the library. The problem size is
-fixed as N grows (strong scaling); `value` is the whole-job rate.
+runs inside the library over one of its data planes: RCCL all-to-all(v) over
+xGMI, IPC peer writes from the stage kernels, or relay routing through idle
+GPUs. Before the timed loop every eligible plane is timed on a few steps
+(config.planes_ms) and the headline runs on the fastest (config.plane_choice;
+--plane forces one). The problem size is fixed as N grows (strong scaling);
+`value` is the whole-job rate.
 """
 from __future__ import annotations
 
@@ -104,9 +108,13 @@ def parse():
                     help="backward+forward pairs of transform 0 timed per stage after the "
                          "timed loop (0 = no stage profile)")
     ap.add_argument("--planes-probe", type=int, default=1,
-                    help="N > 1: after the timed loop, time a few steps (one transform per step) on "
-                         "every eligible data plane (rccl / ipc / relay) and record them in "
-                         "config.planes_ms; the headline stays on the default plane")
+                    help="N > 1: before the timed loop, time a few steps (one transform per step) on "
+                         "every eligible data plane (rccl / ipc / relay), record them in "
+                         "config.planes_ms and run the headline on the fastest (--plane auto)")
+    ap.add_argument("--plane", default="auto", choices=["auto", "default", "rccl", "ipc", "relay"],
+                    help="N > 1: data plane of the headline transforms: auto = the fastest of the "
+                         "probe (the library's default if the probe is off), default = the "
+                         "library's own choice, or one plane forced")
     ap.add_argument("--sync", default="stream", choices=["stream", "call"],
                     help="stream: transforms are stream-ordered on torch's current stream (no host "
                          "wait per call; the timed loop still ends with a device synchronize); "
@@ -148,6 +156,40 @@ def _roundtrip_gpu(sp, ts, vals, outs, r2c):
     return worst
 
 
+def _plane_env(name, shared):
+    """The library's plane switches (read at grid setup) that select a data plane;
+    ranks sharing a GPU relay through virtual relays (rehearsal)."""
+    return {"rccl": {"SPFFT_GPU_EXCHANGE": "rccl", "SPFFT_RELAY": "0"},
+            "ipc": {"SPFFT_GPU_EXCHANGE": "ipc", "SPFFT_RELAY": "0"},
+            "relay": {"SPFFT_GPU_EXCHANGE": "", "SPFFT_RELAY": "force" if shared else "auto"}}.get(name, {})
+
+
+def _gather_devices(torch, dev, dist, world):
+    prop = torch.cuda.get_device_properties(dev)
+    mine = f"{prop.pci_domain_id:04x}:{prop.pci_bus_id:02x}:{prop.pci_device_id:02x}"
+    if dist is None:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def _choose_plane(requested, planes_ms):
+    """The headline's data plane: the forced one, or (auto) the fastest plane of the
+    probe that really ran as itself (a plane that fell back to another is not a
+    candidate); the library's default when nothing was probed."""
+    if requested not in ("auto",):
+        return {"plane": requested, "basis": "--plane"}
+    if any(os.environ.get(k) for k in ("SPFFT_GPU_EXCHANGE", "SPFFT_RELAY")):
+        return {"plane": "default", "basis": "the plane switches set in the environment"}
+    ok = {k: v["ms_per_step"] for k, v in (planes_ms or {}).items()
+          if "ms_per_step" in v and v.get("plane") == k}
+    if not ok:
+        return {"plane": "default", "basis": "no probe result: the library's default plane"}
+    best = min(ok, key=ok.get)
+    return {"plane": best, "basis": "fastest of planes_ms", "ms_per_step": ok[best]}
+
+
 def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, warmup=2):
     """ms per step (one backward + forward of one transform) on every eligible data
     plane, each forced through the library's plane switches (read at grid setup):
@@ -156,9 +198,7 @@ def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, war
     is recorded with its error (the failure is agreed on by every rank)."""
     import time as _t
     import torch
-    planes = {"rccl": {"SPFFT_GPU_EXCHANGE": "rccl", "SPFFT_RELAY": "0"},
-              "ipc": {"SPFFT_GPU_EXCHANGE": "ipc", "SPFFT_RELAY": "0"},
-              "relay": {"SPFFT_GPU_EXCHANGE": "", "SPFFT_RELAY": "force" if shared else "auto"}}
+    planes = {name: _plane_env(name, shared) for name in ("rccl", "ipc", "relay")}
     out = {}
     for name, env in planes.items():
         if name == "rccl" and shared and os.environ.get("SPFFT_RCCL_VIRTUAL_HOSTS") != "1":
@@ -292,6 +332,15 @@ def main():
                                  transform_type=ttype, exchange_type=exch, single=single)
         return setup.grid, setup.transform, setup.indices, setup.z_length
 
+    # N > 1: time every eligible data plane first and run the headline on the
+    # fastest (the library's plane switches are read at grid setup)
+    planes_ms, plane_choice = None, None
+    if world > 1:
+        shared = len(set(_gather_devices(torch, dev, dist, world))) < world
+        if a.planes_probe:
+            planes_ms = _probe_planes(make_transform, dev, cdtype, world, shared, dist)
+        plane_choice = _choose_plane(a.plane, planes_ms)
+        os.environ.update(_plane_env(plane_choice["plane"], shared))
     T = max(1, a.transforms)
     made = [make_transform() for _ in range(T)]
     grids = [m[0] for m in made]
@@ -303,12 +352,7 @@ def main():
     plane_info = grid.data_plane_info if world > 1 else {"kind": "none"}
     # every GPU the job touched: the ranks' devices (PCI locations, gathered) and
     # any relay GPUs the data plane uses besides them
-    prop = torch.cuda.get_device_properties(dev)
-    my_dev = f"{prop.pci_domain_id:04x}:{prop.pci_bus_id:02x}:{prop.pci_device_id:02x}"
-    rank_devs = [my_dev]
-    if dist is not None:
-        rank_devs = [None] * world
-        dist.all_gather_object(rank_devs, my_dev)
+    rank_devs = _gather_devices(torch, dev, dist, world)
     touched = list(dict.fromkeys(rank_devs + list(plane_info.get("devices", []))))
     if a.streams == "auto":
         a.streams = "one" if world == 1 else "per-transform"
@@ -409,9 +453,6 @@ def main():
         model = _model(stages, xstats["max_bytes_sent_per_rank"], world, chunks, blocks, relays, link)
         model["peer_writes"] = peer_writes
         model["shared_device"] = n_devices < world
-    planes_ms = None
-    if world > 1 and a.planes_probe:
-        planes_ms = _probe_planes(make_transform, dev, cdtype, world, n_devices < world, dist)
     ms_per_step = 1e3 * elapsed / a.steps
     rate = 2.0 * T * a.steps / elapsed
     # the reference's FFT calls alone (rocFFT via
@@ -466,9 +507,9 @@ def main():
                 "exchange_stats": xstats,
                 "model_ms": model,
                 "planes_ms": planes_ms,
-                "planes_ms_basis": ("one transform per step, 2 warmup + 5 timed steps per plane after "
-                                    "the timed loop; the headline uses the default plane"
-                                    if planes_ms else None),
+                "planes_ms_basis": ("one transform per step, 2 warmup + 5 timed steps per plane, "
+                                    "before the timed loop" if planes_ms else None),
+                "plane_choice": plane_choice,
                 "step": ("1 backward + 1 forward transform" if T == 1 else
                          f"multi_transform backward + forward of {T} independent transforms"),
             },
