@@ -1256,11 +1256,12 @@ public:
       const long long saved = minBytes_;
       minBytes_ = 0;  // every route, whatever the production threshold
       // the registered path the executors use: device barriers, plane stream
+      const std::size_t before = reg_.size();
       const int id = register_exchange(0, xs);
       minBytes_ = saved;
       exchange_registered(id, nullptr, nullptr);
       gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-      reg_.pop_back();
+      if (reg_.size() > before) reg_.pop_back();  // (its split ignored the threshold)
       std::vector<unsigned long long> got(pattern.size());
       gpu_check(hipMemcpy(got.data(), recv, got.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy");
       for (int q = 0; q < P_ && ok; ++q)
@@ -1432,12 +1433,19 @@ public:
     DeviceGuard guard(device_);
     int W = 0;
     const std::vector<Transfer> all = gather_lists(xs, false, &W);
+    // the same exchange registered again (another transform of the grid with
+    // the same plan): every rank sees the same gathered lists, so every rank
+    // reuses the same entry
+    for (std::size_t i = 0; i < reg_.size(); ++i)
+      if (reg_[i].sendSlot == sendSlot && same_lists(reg_[i].lists, all)) return static_cast<int>(i);
     std::vector<dev::CopySeg> push, pull;
     const char* s = static_cast<const char*>(local_buffer(sendSlot));
     char* r = static_cast<char*>(local_buffer(1 - sendSlot));
     if (!xs.empty() && (!s || !r)) throw InternalError();
     build_segs(s, r, sendSlot, xs, all, W, push, pull);
     Registered g;
+    g.sendSlot = sendSlot;
+    g.lists = all;
     auto up = [](std::unique_ptr<DeviceBuffer>& b, const std::vector<dev::CopySeg>& v) {
       if (v.empty()) return;
       b.reset(new DeviceBuffer(v.size() * sizeof(dev::CopySeg)));
@@ -1552,7 +1560,17 @@ private:
     std::unique_ptr<DeviceBuffer> push, pull;
     int nPush = 0, nPull = 0;
     long long chPush = 0, chPull = 0;
+    int sendSlot = 0;
+    std::vector<Transfer> lists;  // every rank's list as gathered (identity of the entry)
   };
+  static bool same_lists(const std::vector<Transfer>& a, const std::vector<Transfer>& b) {
+    if (a.size() != b.size()) return false;
+    for (std::size_t i = 0; i < a.size(); ++i)
+      if (a[i].kind != b[i].kind || a[i].peer != b[i].peer || a[i].offset != b[i].offset ||
+          a[i].dstOffset != b[i].dstOffset || a[i].bytes != b[i].bytes)
+        return false;
+    return true;
+  }
 
   std::shared_ptr<Communicator> comm_;
   int device_, me_, P_, K_;
