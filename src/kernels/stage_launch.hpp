@@ -42,8 +42,9 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
     // 64.9 -> 69.3 us per transform at 256^3 fp64 T = 4; profiles/r6/zb2)
     const ZArgs b = z_args_for_lds(a, lds, lines, &ldsTotal);
     prepare_kernel(k, ldsTotal);
-    hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, b,
-                       in, values, scale, tw);
+    const unsigned nb = static_cast<unsigned>(ceil_div(a.numSticks - a.stickBegin, lines));
+    hipLaunchKernelGGL(k, dim3(nb, 1, batch_dim(b.batch)), dim3(threads), ldsTotal, stream, eng, b, in, values,
+                       scale, tw);
     gpu_check_launch("z_forward", stream);
   });
 }
