@@ -1079,23 +1079,32 @@ struct BarrierRounds {
 // share per peer, N - 1 in all): the exchange takes (N - 1) / (N - 1 + K) of
 // the direct-only link time, 1/7 at N = 2 on 8 GPUs, 3/7 at N = 4.
 //
-// Two host-synchronous phases per exchange, each one multi-segment copy
-// launch on the caller's device (kernels/relay_copy.hip):
+// Two phases per exchange, each one multi-segment copy launch on the caller's
+// device (kernels/relay_copy.hip):
 //  1. push: the relay shares into this rank's relay buffers on the idle GPUs
 //     (memory this process allocates there, from the IPC arena, and exports
 //     to the peers);
-//  2. pull, after a communicator barrier: each receiver copies its direct part
-//     out of the sender's send side and its relay shares out of the senders'
-//     relay buffers; a second barrier frees the buffers.
+//  2. pull, after a barrier: each receiver copies its direct part out of the
+//     sender's send side and its relay shares out of the senders' relay
+//     buffers; a second barrier frees the buffers.
+// The executors register their exchanges at plan time (register_exchange:
+// the ranks' transfer lists are gathered once, the split and both copy
+// tables stay on the device); a registered exchange is stream-ordered: push,
+// device barrier round (BarrierRounds, the peer plane's barrier kernel), pull,
+// device barrier round, on one ordered stream per member set and device.
+// Unregistered exchanges gather the lists per call and separate the phases
+// with host barriers.
 // No GPU writes into another rank's GPU memory: a receiver's L2 may hold lines
 // of its own buffers from an earlier read, which a remote store would leave
 // stale. Remote memory is only read (its lines are dropped by the copy
 // kernel's system-scope acquire) or written on an idle GPU that runs no
 // kernels.
-// Every rank computes every rank's split from the allgathered transfer lists,
+// Every rank computes every rank's split from the gathered transfer lists,
 // so the layouts agree without further messages. Shares are multiples of 16
-// bytes; messages below SPFFT_RELAY_MIN_BYTES (default 1 MiB) go direct only.
-// SPFFT_RELAY: "auto" (default: on when idle GPUs are visible), "0" off,
+// bytes; messages below SPFFT_RELAY_MIN_BYTES (default 1 MiB, rank 0's value)
+// go direct only.
+// SPFFT_RELAY: "auto" (default: through GPUs of the node that are idle, when
+// the group is the node's whole job and the model says it pays), "0" off,
 // "force" (relay through K = SPFFT_RELAY_VIRTUAL virtual relays on the rank's
 // own GPU: exercises the layouts and phases on a one-GPU box).
 class RelayDeviceComm : public DeviceComm {
