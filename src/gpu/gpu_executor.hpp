@@ -205,6 +205,7 @@ private:
   void register_exchanges();
   int bwdId_ = -1, fwdId_ = -1;  // registered unpipelined exchanges
   int plainHandoff_ = 0;         // backward stick hand-off through the Infinity Cache
+  long long peerStickStride_ = 0;  // peer writes: stick row stride of the stick side
   int exchChunks_ = 1;   // K
   int stickBlocks_ = 1;  // I
   bool pipelined() const { return exchChunks_ > 1 || stickBlocks_ > 1; }
