@@ -303,3 +303,28 @@ def test_release_library_has_no_test_hooks():
     tsyms = subprocess.run([nm, "-D", "--defined-only", TESTING_LIB], capture_output=True, text=True,
                            check=True).stdout
     assert "spfft_amd_test_comm_shm_check" in tsyms and "spfft_amd_test_fault_injection" in tsyms
+
+
+def test_bench_plane_choice(monkeypatch):
+    """bench.py N > 1: the headline runs on the fastest probed plane that really ran
+    as itself (a plane that fell back to another is no candidate); --plane forces one;
+    plane switches set in the environment keep the library's own choice."""
+    import importlib.util
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(repo, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    for k in ("SPFFT_GPU_EXCHANGE", "SPFFT_RELAY"):
+        monkeypatch.delenv(k, raising=False)
+    probe = {"rccl": {"ms_per_step": 1.2, "plane": "rccl"},
+             "ipc": {"ms_per_step": 0.9, "plane": "ipc"},
+             "relay": {"ms_per_step": 0.5, "plane": "rccl"}}  # relay fell back to RCCL
+    assert b._choose_plane("auto", probe)["plane"] == "ipc"
+    assert b._choose_plane("rccl", probe)["plane"] == "rccl"
+    assert b._choose_plane("auto", {"ipc": {"error": "MPIError"}})["plane"] == "default"
+    assert b._choose_plane("auto", None)["plane"] == "default"
+    monkeypatch.setenv("SPFFT_RELAY", "force")
+    assert b._choose_plane("auto", probe)["plane"] == "default"
+    assert b._plane_env("relay", True)["SPFFT_RELAY"] == "force"
+    assert b._plane_env("relay", False)["SPFFT_RELAY"] == "auto"
