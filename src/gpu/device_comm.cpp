@@ -1210,8 +1210,16 @@ public:
       throw MPIError();
     }
     gpu_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    // device barrier rounds and the plane's stream (registered exchanges)
-    bar_.setup(*comm_, device);
+    // device barrier rounds and the plane's stream (registered exchanges); a
+    // failed setup (agreed by every rank) unmaps the peers' buffers before the
+    // constructor unwinds
+    try {
+      bar_.setup(*comm_, device);
+    } catch (...) {
+      for (void* p : opened_) ipc_close(p);
+      opened_.clear();
+      throw;
+    }
     // one ordered stream per member set and device, shared by every relay
     // plane of the process: the barrier rounds of all its grids run in host
     // issue order, the order every rank issues them in (transforms are
