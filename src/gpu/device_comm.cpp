@@ -615,7 +615,18 @@ public:
       timeoutTicks_ = static_cast<long long>(peer_timeout_seconds() * 1e3 * std::max(rateKHz, 1));
       comm_->barrier();  // every flag array is zeroed before the first barrier round
       devices_ = group_devices(*comm_, device);
-      self_test();
+      try {
+        self_test();
+      } catch (...) {
+        // (every rank fails together; the destructor does not run for a
+        // constructor that throws)
+        for (void* p : opened_) ipc_close(p);
+        opened_.clear();
+        if (flags_) flags_->discard();
+        if (orderEv_) (void)hipEventDestroy(orderEv_);
+        if (failHost_) (void)hipHostFree(failHost_);
+        throw;
+      }
       return;
     } else {
       // in-process groups meet on the host: ranks of one process share its few
