@@ -46,12 +46,6 @@ struct ZArgs {
   // otherwise, per plane z two entries: (base, stride) of its exchange segment,
   // element (stick s, plane z) at base + s * stride (base includes z)
   const long long* zTab;
-  // z backward: streaming (non-temporal) value loads, set for batched
-  // launches, whose several inputs cannot stay in the Infinity Cache anyway
-  // (plain loads keep a single transform's values resident across calls: 63
-  // us plain vs 79 us nt at 256^3 fp64 T = 1; batched 75.6 plain vs 59-70 us
-  // nt per transform; profiles/r6/zb, zb2)
-  int ntValues;
   int plainSticks;  // backward: stick stores with the default cache policy (see GpuExecutor)
   BatchPtrs batch;
 };

@@ -32,19 +32,21 @@ __device__ __forceinline__ void st_stream(cx<T>* p, cx<T> v) {
   __builtin_nontemporal_store(w, reinterpret_cast<V*>(p));
 }
 // Stick-side accesses of the backward z -> y hand-off: streaming (nt), or with
-// the default cache policy (plain: the lines stay in the 256 MB Infinity
-// Cache, where the y stage finds them) when `plain` is set (GpuExecutor).
-template <typename T>
-__device__ __forceinline__ cx<T> ld_stick(const cx<T>* p, int plain) {
-  if (plain) return *p;
-  return ld_stream(p);
+// the default cache policy (Plain: the lines stay in the 256 MB Infinity
+// Cache, where the y stage finds them; GpuExecutor::plainHandoff_). Plain is a
+// template parameter of the kernels, not a run-time flag: with a run-time
+// branch the compiler merged the two stores (loads) of the branch into one and
+// dropped the non-temporal hint, so every stick access ran plain (512^3 R2C
+// fp32 z backward 146 -> 206 us, z forward 112 -> 129 us; profiles/r6/ntmerge).
+template <bool Plain, typename T>
+__device__ __forceinline__ cx<T> ld_stick(const cx<T>* p) {
+  if constexpr (Plain) return *p;
+  else return ld_stream(p);
 }
-template <typename T>
-__device__ __forceinline__ void st_stick(cx<T>* p, cx<T> v, int plain) {
-  if (plain)
-    *p = v;
-  else
-    st_stream(p, v);
+template <bool Plain, typename T>
+__device__ __forceinline__ void st_stick(cx<T>* p, cx<T> v) {
+  if constexpr (Plain) *p = v;
+  else st_stream(p, v);
 }
 // The [z][column][y] intermediate is streamed like the rest.
 template <typename T>
@@ -778,20 +780,19 @@ __device__ __forceinline__ int desc_offset(const StickDesc& q, int z) {
   return -1;
 }
 
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Plain>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_backward_desc_kernel(Eng eng, ZArgs a, const cx<T>* __restrict__ values,
                            BT* __restrict__ out, const cx<T>* __restrict__ tw) {
   SPFFT_LDS_DECL(T);
   SPFFT_BATCH_SELECT(a, values, out);
-  const bool ntv = a.ntValues != 0;
   const int B = eng.lines();
   const int n = eng.n();
   const int s0 = a.stickBegin + block_tile_x() * B;
   const int nl = min(B, a.numSticks - s0);
   const ZSeg seg(a, reinterpret_cast<char*>(lds) + zseg_lds_offset(eng.lds_bytes(), B), eng.n());
   auto store = [&](int b, int pos, cx<T> v) {
-    if (b < nl) st_stick(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v), a.plainSticks);
+    if (b < nl) st_stick<Plain>(&out[seg.at(s0 + b, pos)], cvt<typename BT::value_type>(v));
   };
   StickDesc* d = reinterpret_cast<StickDesc*>(reinterpret_cast<char*>(lds) + eng.lds_bytes());
   for (int b = threadIdx.x; b < nl; b += blockDim.x) d[b] = a.desc[s0 + b];
@@ -835,8 +836,9 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const bool in0 = j0 < static_cast<unsigned>(len0);
       const bool in1 = j1 < static_cast<unsigned>(len1);
       const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
-      if (ntv) return (in0 || in1) ? ld_stream(&vals[j]) : czero<T>();
-      return (in0 || in1) ? ld_values(&vals[j]) : czero<T>();
+      // streamed value loads: 256^3 fp64 79.2 -> 63.4 us, 512^3 R2C fp32 219 ->
+      // 133 us, fp32 256^3 neutral (T = 1, same box; profiles/r6/ntmerge)
+      return (in0 || in1) ? ld_stream(&vals[j]) : czero<T>();
     }, store);
   }
 }
@@ -881,11 +883,11 @@ __global__ void __launch_bounds__(Eng::kBlock)
       // element a constant offset from it; no segment-mode branch and no 64-bit
       // multiply per element (the other modes below read a table per position)
       const BT* row = in + static_cast<long long>(ls) * seg.stride + Eng::F::lane_pos();
-      eng.global_to_global(lds, tw, [&](int, int, int off) -> cx<T> { return cvt<T>(ld_stick(&row[off], a.plainSticks)); },
+      eng.global_to_global(lds, tw, [&](int, int, int off) -> cx<T> { return cvt<T>(ld_stream(&row[off])); },
                            store);
     } else {
       eng.global_to_global(lds, tw, [&](int, int pos) -> cx<T> {
-        return cvt<T>(ld_stick(&in[seg.at(ls, pos)], a.plainSticks));
+        return cvt<T>(ld_stream(&in[seg.at(ls, pos)]));
       }, store);
     }
   } else {
@@ -1052,7 +1054,7 @@ constexpr bool y_table() {
 // loads straight from the stick side — consecutive lanes read consecutive z
 // of one stick (coalesced) — with no LDS staging of the input. The x = 0
 // column of an R2C transform is gathered into LDS for the hermitian fill.
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool Plain>
 __global__ void __launch_bounds__(Eng::kBlock)
     y_backward_kernel(Eng eng, YArgs a, const BT* __restrict__ in, cx<T>* __restrict__ inter,
                       const cx<T>* __restrict__ tw) {
@@ -1073,7 +1075,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
       // zero source instead: fp32 512^3 R2C y backward 228 -> 212 us, 256^3 neutral;
       // profiles/r5/ab/ymask)
       cx<T> v = czero<T>();
-      if (base != kNoBase && b < zl) v = cvt<T>(ld_stick(in + (base + z0 + b), a.plainSticks));
+      if (base != kNoBase && b < zl) v = cvt<T>(ld_stick<Plain>(in + (base + z0 + b)));
       return v;
     } else {
       long long base;
@@ -1149,7 +1151,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
     stage_rows(eng, lds, zl, n, rows);
     eng.lds_to_global(lds, tw, [&](int b, int, cx<T> v) {
       const long long base = bases[slot++];
-      if (base != kNoBase && b < zl) st_stick(&out[base + z0 + b], cvt<typename BT::value_type>(v), a.plainSticks);
+      if (base != kNoBase && b < zl) st_stream(&out[base + z0 + b], cvt<typename BT::value_type>(v));
     });
     return;
   }

@@ -19,10 +19,12 @@ void launch_z_backward(const ZArgs& a, const cx<T>* values, BT* out, const cx<T>
   if (a.numSticks <= a.stickBegin) return;
   with_engine<T, +1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     using E = decltype(eng);
-    auto k = a.desc ? z_backward_desc_kernel<E, T, BT> : z_backward_kernel<E, T, BT>;
+    // (plain stick stores only where the executor asks for them: plainSticks)
+    const bool plain = a.plainSticks != 0;
+    auto k = !a.desc ? z_backward_kernel<E, T, BT>
+             : plain ? z_backward_desc_kernel<E, T, BT, true> : z_backward_desc_kernel<E, T, BT, false>;
     std::size_t ldsTotal = 0;
-    ZArgs b = z_args_for_lds(a, lds, lines, &ldsTotal);
-    b.ntValues = a.batch.count > 1 ? 1 : 0;
+    const ZArgs b = z_args_for_lds(a, lds, lines, &ldsTotal);
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, dim3(ceil_div(a.numSticks - a.stickBegin, lines), 1, batch_dim(a.batch)), dim3(threads),
                        ldsTotal, stream, eng, b, values, out, tw);
@@ -54,7 +56,7 @@ void launch_y_backward(const YArgs& a, const BT* in, cx<T>* inter, const cx<T>* 
                        hipStream_t stream) {
   if (a.colEnd <= a.colBegin || a.L <= a.zBegin) return;
   with_engine<T, +1, true>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
-    auto k = y_backward_kernel<decltype(eng), T, BT>;
+    auto k = a.plainSticks ? y_backward_kernel<decltype(eng), T, BT, true> : y_backward_kernel<decltype(eng), T, BT, false>;
     const std::size_t ldsTotal = lds + col_entries_lds(a, true, y_table<decltype(eng), true>());
     prepare_kernel(k, ldsTotal);
     hipLaunchKernelGGL(k, y_grid(a.colEnd - a.colBegin, ceil_div(a.L - a.zBegin, lines), batch_dim(a.batch)), dim3(threads), ldsTotal, stream, eng, a,
