@@ -305,6 +305,34 @@ def test_release_library_has_no_test_hooks():
     assert "spfft_amd_test_comm_shm_check" in tsyms and "spfft_amd_test_fault_injection" in tsyms
 
 
+def test_stage_kernels_keep_nt_hints():
+    """The z/y stage kernels' stick-side accesses keep the cache policy they were
+    written with in the built gfx950 code: streaming (nt) stores in the z backward
+    kernels unless instantiated Plain, nt stick stores in the y forward kernels. A
+    run-time plain/nt branch had the compiler drop the hints (profiles/r6/ntmerge);
+    tools/nt_audit.py reads the library's code objects."""
+    import os
+    import shutil
+    import sys
+    from spfft_amd.ops._lib import NATIVE_DIR
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import nt_audit
+    if not shutil.which("objcopy") or not nt_audit._tool("clang-offload-bundler") or not nt_audit._tool("llvm-objdump"):
+        pytest.skip("objcopy / clang-offload-bundler / llvm-objdump not available")
+    lib = os.path.join(NATIVE_DIR, "libspfft_amd.so")
+    res = nt_audit.audit(lib, r"(z_backward_desc|y_forward)_kernel.*CtEngI[fd]Li(256|512)E",
+                         needles=(b"z_backward_desc_kernel", b"y_forward_kernel"))
+    zb = {k: c for k, c in res.items() if "z_backward_desc" in k}
+    yf = {k: c for k, c in res.items() if "y_forward" in k}
+    assert len(zb) >= 8 and len(yf) >= 4, sorted(res)
+    for k, c in zb.items():
+        plain = "Lb1EEEvT_" in k  # the trailing bool template argument (Plain)
+        assert c["st"] > 0 and c["st_nt"] == (0 if plain else c["st"]), (k, c)
+        assert c["ld_nt"] > 0, (k, c)  # streamed value loads
+    for k, c in yf.items():
+        assert c["st"] > 0 and c["st_nt"] == c["st"], (k, c)
+
+
 def test_bench_plane_choice(monkeypatch):
     """bench.py N > 1: the headline runs on the fastest probed plane that really ran
     as itself (a plane that fell back to another is no candidate); --plane forces one;
