@@ -859,6 +859,11 @@ dev::ZArgs GpuExecutor<T>::zargs() const {
   a.single = p.size == 1 ? 1 : 0;
   a.stickStride = layout_.stickStride[0];
   a.zTab = zTab_ ? zTab_->data<long long>() : nullptr;
+  // Forward value stores streamed when one transform's values outgrow what the
+  // 256 MB Infinity Cache keeps: 512^3 R2C fp32 (282 MB of values) T = 4 1870
+  // -> 1900 transforms/s; 256^3 (70 / 140 MB) kept plain, nt there lost 2-3%
+  // (profiles/r6/ntmerge/zf_values_ab.txt)
+  a.ntValueStores = static_cast<double>(p.numLocalElements) * sizeof(cx<T>) > 192.0 * (1 << 20) ? 1 : 0;
   return a;
 }
 

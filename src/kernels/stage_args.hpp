@@ -47,6 +47,9 @@ struct ZArgs {
   // element (stick s, plane z) at base + s * stride (base includes z)
   const long long* zTab;
   int plainSticks;  // backward: stick stores with the default cache policy (see GpuExecutor)
+  // forward: streaming (nt) value stores, for value arrays larger than the
+  // Infinity Cache can keep (GpuExecutor)
+  int ntValueStores;
   BatchPtrs batch;
 };
 

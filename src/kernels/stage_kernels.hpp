@@ -843,7 +843,7 @@ __global__ void __launch_bounds__(Eng::kBlock)
   }
 }
 
-template <class Eng, typename T, typename BT>
+template <class Eng, typename T, typename BT, bool NtValues>
 __global__ void __launch_bounds__(Eng::kBlock)
     z_forward_desc_kernel(Eng eng, ZArgs a, const BT* __restrict__ in, cx<T>* __restrict__ values,
                           T scale, const cx<T>* __restrict__ tw) {
@@ -872,7 +872,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
       const bool in0 = j0 < static_cast<unsigned>(len0);
       const bool in1 = j1 < static_cast<unsigned>(len1);
       const int j = in0 ? static_cast<int>(j0) : len0 + static_cast<int>(j1);
-      if (in0 || in1) st_values(&vals[j], spfft::scale(v, scale));
+      if (in0 || in1) {
+        if constexpr (NtValues) st_stream(&vals[j], spfft::scale(v, scale));
+        else st_values(&vals[j], spfft::scale(v, scale));
+      }
     };
     // Lanes past the last stick load a valid stick (min(lb, nl - 1)) and store
     // nothing (len0 = len1 = 0): no guard per element. Loads only the lane's own
@@ -901,7 +904,10 @@ __global__ void __launch_bounds__(Eng::kBlock)
       if (b >= nl) return;
       const StickDesc& q = d[b];
       const int j = desc_offset(q, pos);
-      if (j >= 0) st_values(&values[q.valueStart + j], spfft::scale(v, scale));
+      if (j >= 0) {
+        if constexpr (NtValues) st_stream(&values[q.valueStart + j], spfft::scale(v, scale));
+        else st_values(&values[q.valueStart + j], spfft::scale(v, scale));
+      }
     });
   }
 }

@@ -38,10 +38,9 @@ void launch_z_forward(const ZArgs& a, const BT* in, cx<T>* values, T scale, cons
   if (a.numSticks <= a.stickBegin) return;
   with_engine<T, -1>(a.n, [&](auto eng, int threads, int lines, std::size_t lds) {
     using E = decltype(eng);
-    auto k = a.desc ? z_forward_desc_kernel<E, T, BT> : z_forward_kernel<E, T, BT>;
+    auto k = !a.desc ? z_forward_kernel<E, T, BT>
+             : a.ntValueStores ? z_forward_desc_kernel<E, T, BT, true> : z_forward_desc_kernel<E, T, BT, false>;
     std::size_t ldsTotal = 0;
-    // (plain value stores also in batched launches: nt stores measured slower,
-    // 64.9 -> 69.3 us per transform at 256^3 fp64 T = 4; profiles/r6/zb2)
     const ZArgs b = z_args_for_lds(a, lds, lines, &ldsTotal);
     prepare_kernel(k, ldsTotal);
     const unsigned nb = static_cast<unsigned>(ceil_div(a.numSticks - a.stickBegin, lines));
