@@ -111,6 +111,8 @@ def parse():
                     help="N > 1: before the timed loop, time a few steps (one transform per step) on "
                          "every eligible data plane (rccl / ipc / relay), record them in "
                          "config.planes_ms and run the headline on the fastest (--plane auto)")
+    ap.add_argument("--probe-planes", default="rccl,ipc,relay",
+                    help="comma-separated data planes the probe times (--planes-probe 1)")
     ap.add_argument("--plane", default="auto", choices=["auto", "default", "rccl", "ipc", "relay"],
                     help="N > 1: data plane of the headline transforms: auto = the fastest of the "
                          "probe (the library's default if the probe is off), default = the "
@@ -190,7 +192,8 @@ def _choose_plane(requested, planes_ms):
     return {"plane": best, "basis": "fastest of planes_ms", "ms_per_step": ok[best]}
 
 
-def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, warmup=2):
+def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, warmup=2,
+                  names=("rccl", "ipc", "relay")):
     """ms per step (one backward + forward of one transform) on every eligible data
     plane, each forced through the library's plane switches (read at grid setup):
     rccl (not between ranks that share a GPU), ipc (peer writes) and relay (idle GPUs
@@ -198,7 +201,7 @@ def _probe_planes(make_transform, dev, cdtype, world, shared, dist, steps=5, war
     is recorded with its error (the failure is agreed on by every rank)."""
     import time as _t
     import torch
-    planes = {name: _plane_env(name, shared) for name in ("rccl", "ipc", "relay")}
+    planes = {name: _plane_env(name, shared) for name in names}
     out = {}
     for name, env in planes.items():
         if name == "rccl" and shared and os.environ.get("SPFFT_RCCL_VIRTUAL_HOSTS") != "1":
@@ -338,7 +341,8 @@ def main():
     if world > 1:
         shared = len(set(_gather_devices(torch, dev, dist, world))) < world
         if a.planes_probe:
-            planes_ms = _probe_planes(make_transform, dev, cdtype, world, shared, dist)
+            planes_ms = _probe_planes(make_transform, dev, cdtype, world, shared, dist,
+                                      names=tuple(x for x in a.probe_planes.split(",") if x))
         plane_choice = _choose_plane(a.plane, planes_ms)
         os.environ.update(_plane_env(plane_choice["plane"], shared))
     T = max(1, a.transforms)

@@ -22,7 +22,8 @@ def build_variant(name, flags):
         subprocess.run(["cmake", "-S", REPO, "-B", bdir, "-G", "Ninja", "-DCMAKE_BUILD_TYPE=Release",
                         f"-DCMAKE_C_COMPILER={clang}/clang", f"-DCMAKE_CXX_COMPILER={clang}/clang++",
                         f"-DCMAKE_HIP_COMPILER={clang}/clang++", "-DCMAKE_HIP_ARCHITECTURES=gfx950",
-                        f"-DCMAKE_HIP_FLAGS={' '.join(flags)}"], check=True, stdout=subprocess.DEVNULL)
+                        f"-DCMAKE_HIP_FLAGS={' '.join(flags)}", f"-DCMAKE_CXX_FLAGS={' '.join(flags)}"],
+                       check=True, stdout=subprocess.DEVNULL)
     subprocess.run(["cmake", "--build", bdir, "--target", "spfft_amd", "-j", "16"], check=True,
                    stdout=subprocess.DEVNULL)
     out = os.path.join(REPO, "spfft_amd", "_native", "variants")
