@@ -90,6 +90,7 @@ struct NcclChannel {
   std::unique_ptr<GpuEvent> in, out;
   std::mutex m;
   bool aborted = false;
+  bool highPriority = true;  // channel stream priority (see channel_priority)
   std::string detail;  // why initialisation failed (comm == nullptr)
 
   ~NcclChannel() {
@@ -152,7 +153,7 @@ struct NcclChannel {
       comm = nullptr;
       return;
     }
-    stream.reset(new GpuStream(true));
+    stream.reset(new GpuStream(highPriority));
     in.reset(new GpuEvent());
     out.reset(new GpuEvent());
   }
@@ -539,9 +540,9 @@ struct PeerChannel {
   hipEvent_t in = nullptr, out = nullptr;
   std::mutex m;
 
-  explicit PeerChannel(int dev) : device(dev) {
+  PeerChannel(int dev, bool highPriority) : device(dev) {
     DeviceGuard guard(device);
-    stream.reset(new GpuStream(true));
+    stream.reset(new GpuStream(highPriority));
     gpu_check(hipEventCreateWithFlags(&in, hipEventDisableTiming), "hipEventCreateWithFlags");
     gpu_check(hipEventCreateWithFlags(&out, hipEventDisableTiming), "hipEventCreateWithFlags");
   }
@@ -558,13 +559,13 @@ std::map<std::string, std::weak_ptr<PeerChannel>>& peer_channel_registry() {
   return *r;
 }
 
-std::shared_ptr<PeerChannel> acquire_peer_channel(const std::string& key, int device) {
+std::shared_ptr<PeerChannel> acquire_peer_channel(const std::string& key, int device, bool highPriority) {
   std::lock_guard<std::mutex> lock(gPeerChannelMutex);
   auto& reg = peer_channel_registry();
   auto it = reg.find(key);
   std::shared_ptr<PeerChannel> ch = it != reg.end() ? it->second.lock() : nullptr;
   if (!ch) {
-    ch = std::make_shared<PeerChannel>(device);
+    ch = std::make_shared<PeerChannel>(device, highPriority);
     reg[key] = ch;
   }
   return ch;
@@ -591,7 +592,8 @@ public:
   // and the grid switches to them (local_buffer); `bytes` are the sides'
   // sizes.
   PeerDeviceComm(const std::shared_ptr<Communicator>& comm, int device, void* const buffers[2],
-                 const std::size_t bytes[2], bool ipc, const std::string& channelKey)
+                 const std::size_t bytes[2], bool ipc, const std::string& channelKey,
+                 bool highPriority = true)
       : comm_(comm), device_(device), me_(comm->rank()), P_(comm->size()), ipc_(ipc) {
     DeviceGuard guard(device);
     gpu_check(hipHostMalloc(reinterpret_cast<void**>(&failHost_), 64,
@@ -606,7 +608,7 @@ public:
       xcdMask_ = dev::xcd_mask(device);
       open_ipc(bytes, fbytes);
       mode_ = peer_barrier_mode();
-      if (mode_ == PeerBarrier::kChannel) channel_ = acquire_peer_channel(channelKey, device);
+      if (mode_ == PeerBarrier::kChannel) channel_ = acquire_peer_channel(channelKey, device, highPriority);
       if (mode_ == PeerBarrier::kStream)
         gpu_check(hipEventCreateWithFlags(&orderEv_, hipEventDisableTiming), "hipEventCreateWithFlags");
       int rateKHz = 0;
@@ -1121,7 +1123,8 @@ struct BarrierRounds {
 class RelayDeviceComm : public DeviceComm {
 public:
   RelayDeviceComm(const std::shared_ptr<Communicator>& comm, int device, const std::size_t bytes[2],
-                  const std::vector<int>& relayDevices, const std::string& channelKey)
+                  const std::vector<int>& relayDevices, const std::string& channelKey,
+                  bool highPriority = true)
       : comm_(comm), device_(device), me_(comm->rank()), P_(comm->size()),
         K_(static_cast<int>(relayDevices.size())), relayDev_(relayDevices) {
     DeviceGuard guard(device);
@@ -1235,7 +1238,7 @@ public:
     // plane of the process: the barrier rounds of all its grids run in host
     // issue order, the order every rank issues them in (transforms are
     // collective), whatever hardware queue the stream lands on
-    channel_ = acquire_peer_channel(channelKey, device);
+    channel_ = acquire_peer_channel(channelKey, device, highPriority);
     gpu_check(hipEventCreateWithFlags(&evIn_, hipEventDisableTiming), "hipEventCreateWithFlags");
     gpu_check(hipEventCreateWithFlags(&evOut_, hipEventDisableTiming), "hipEventCreateWithFlags");
     // the per-exchange host collectives (one allgather, two barriers) through
@@ -1824,7 +1827,8 @@ bool share_channels() {
 // live one (the reuse decision is allgathered, so every rank either reuses or
 // takes part in the new communicator's initialisation).
 std::shared_ptr<NcclChannel> acquire_channel(Communicator* group, const std::string& key, int device,
-                                             int rank, int size, bool selfOnly, int fault) {
+                                             int rank, int size, bool selfOnly, int fault,
+                                             bool highPriority = true) {
   std::shared_ptr<NcclChannel> ch;
   const bool share = share_channels() && fault == 0;
   if (share) {
@@ -1844,6 +1848,7 @@ std::shared_ptr<NcclChannel> acquire_channel(Communicator* group, const std::str
   ch->device = device;
   ch->rank = selfOnly ? 0 : rank;
   ch->size = selfOnly ? 1 : size;
+  ch->highPriority = highPriority;
   ch->init(group, selfOnly, fault);
   if (ch->ok()) {
     ++gChannelsCreated;
@@ -1992,6 +1997,13 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   // once per member set); an xGMI link between distinct GPUs, the GPU's own
   // memory when ranks share one (rehearsals; not used for plane decisions)
   const double linkGBps = oneNode && P > 1 ? node_link_rate(*comm, device, key) : 0.0;
+  // Channel streams are high priority (their rounds and collectives dispatch
+  // ahead of queued stage work) except when ranks share a device: with another
+  // process's high-priority queue on the GPU, both processes' stage kernels ran
+  // about 2x slower, for the rest of the process even after the queue's stream
+  // was destroyed (2 ranks on one GPU, 256^3: 3304 vs 3930-3975 transforms/s;
+  // one process alone shows no effect; profiles/r6/probe_state)
+  const bool highPriority = !sharedDevice;
   auto finish = [&](std::unique_ptr<DeviceComm> dc) {
     dc->set_link_rate(linkGBps, sharedDevice ? "same-device" : "xgmi");
     return dc;
@@ -2016,7 +2028,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
                                                    sharedDevice ? 0.0 : linkGBps);
     if (!relays.empty() && pays) {
       try {
-        return finish(std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays, "relay" + key)));
+        return finish(std::unique_ptr<DeviceComm>(new RelayDeviceComm(comm, device, bytes, relays, "relay" + key, highPriority)));
       } catch (const MPIError&) {
         // every rank agreed on the failure (setup or self-test): the next plane
         if (comm->rank() == 0)
@@ -2028,7 +2040,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
       oneNode && prefer != 1 && (unbuffered || (sharedDevice && fault == 0) || prefer == 2);
   if (peer) {
     try {
-      return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key)));
+      return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key, highPriority)));
     } catch (const PeerSelfTestFailed&) {
       // every rank saw the failure: ranks on distinct devices move the data
       // through RCCL instead (UNBUFFERED included); ranks sharing a device
@@ -2037,7 +2049,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
       if (comm->rank() == 0) std::fprintf(stderr, "spfft: %s; using RCCL\n", error_detail().c_str());
     }
   }
-  auto ch = acquire_channel(comm.get(), key, device, comm->rank(), P, false, fault);
+  auto ch = acquire_channel(comm.get(), key, device, comm->rank(), P, false, fault, highPriority);
   // every rank learns whether every RCCL communicator came up
   int ok = ch->ok() ? 1 : 0;
   std::vector<int> oks(P);
@@ -2056,7 +2068,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   }
   if (comm->rank() == 0)
     std::fprintf(stderr, "spfft: %s; using the peer-write (IPC) data plane\n", why.c_str());
-  return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key)));
+  return finish(std::unique_ptr<DeviceComm>(new PeerDeviceComm(comm, device, buffers, bytes, true, "peer" + key, highPriority)));
 }
 
 }  // namespace spfft

@@ -44,7 +44,16 @@ def main():
     s = torch.cuda.Stream(priority=hi)
     torch.cuda.synchronize()
     res["b_high_prio_alive"] = rate(t, v, o)
-    del s
+    with torch.cuda.stream(s):
+        x = torch.ones(1 << 20, device="cuda")
+        x.mul_(2)
+    torch.cuda.synchronize()
+    res["b2_high_prio_used"] = rate(t, v, o)
+    # the library's own high-priority stream path: the transform on a stream of it
+    t.set_stream(s, synchronous=False)
+    res["b3_transform_on_high_prio"] = rate(t, v, o)
+    t.set_stream(torch.cuda.current_stream(), synchronous=False)
+    del s, x
     gc.collect()
     torch.cuda.synchronize()
     res["c_after_destroy"] = rate(t, v, o)
