@@ -320,17 +320,26 @@ def test_stage_kernels_keep_nt_hints():
     if not shutil.which("objcopy") or not nt_audit._tool("clang-offload-bundler") or not nt_audit._tool("llvm-objdump"):
         pytest.skip("objcopy / clang-offload-bundler / llvm-objdump not available")
     lib = os.path.join(NATIVE_DIR, "libspfft_amd.so")
-    res = nt_audit.audit(lib, r"(z_backward_desc|y_forward)_kernel.*CtEngI[fd]Li(256|512)E",
+    res = nt_audit.audit(lib, r"(z_backward_desc|z_forward_desc|y_forward|y_backward)_kernel.*CtEngI[fd]Li(256|512)E",
                          needles=(b"z_backward_desc_kernel", b"y_forward_kernel"))
     zb = {k: c for k, c in res.items() if "z_backward_desc" in k}
+    zf = {k: c for k, c in res.items() if "z_forward_desc" in k}
     yf = {k: c for k, c in res.items() if "y_forward" in k}
-    assert len(zb) >= 8 and len(yf) >= 4, sorted(res)
+    yb = {k: c for k, c in res.items() if "y_backward" in k}
+    assert len(zb) >= 8 and len(zf) >= 8 and len(yf) >= 4 and len(yb) >= 8, sorted(res)
+    flag = lambda k: "Lb1EEEvT_" in k  # the trailing bool template argument (Plain / NtValues)
     for k, c in zb.items():
-        plain = "Lb1EEEvT_" in k  # the trailing bool template argument (Plain)
-        assert c["st"] > 0 and c["st_nt"] == (0 if plain else c["st"]), (k, c)
+        assert c["st"] > 0 and c["st_nt"] == (0 if flag(k) else c["st"]), (k, c)
         assert c["ld_nt"] > 0, (k, c)  # streamed value loads
+    for k, c in zf.items():
+        assert c["st"] > 0 and c["st_nt"] == (c["st"] if flag(k) else 0), (k, c)
+        assert c["ld_nt"] > 0, (k, c)  # streamed stick loads
     for k, c in yf.items():
         assert c["st"] > 0 and c["st_nt"] == c["st"], (k, c)
+    for k, c in yb.items():
+        if not flag(k):  # the Plain instantiation loads its sticks without the hint
+            twin = yb[k.replace("Lb0EEEvT_", "Lb1EEEvT_")]
+            assert c["ld_nt"] > twin["ld_nt"], (k, c, twin)
 
 
 def test_bench_plane_choice(monkeypatch):
