@@ -1903,6 +1903,10 @@ std::string DeviceComm::info() const {
     j.pop_back();
     j += b;
   }
+  if (channelPriority_ && !j.empty() && j.back() == '}') {
+    j.pop_back();
+    j += std::string(", \"channel_priority\": \"") + channelPriority_ + "\"}";
+  }
   return j;
 }
 
@@ -2006,6 +2010,7 @@ std::unique_ptr<DeviceComm> DeviceComm::create(const std::shared_ptr<Communicato
   const bool highPriority = !sharedDevice;
   auto finish = [&](std::unique_ptr<DeviceComm> dc) {
     dc->set_link_rate(linkGBps, sharedDevice ? "same-device" : "xgmi");
+    dc->set_channel_priority(highPriority);
     return dc;
   };
   // auto relay only when this group is every rank of the job on the node (the

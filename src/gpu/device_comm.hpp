@@ -163,6 +163,8 @@ public:
   virtual std::string info_json() const { return std::string("{\"kind\": \"") + kind() + "\"}"; }
   // info_json() plus "link_GBps_measured" when the link probe ran
   std::string info() const;
+  // priority of the plane's channel streams ("high" / "normal"; DeviceComm::create)
+  void set_channel_priority(bool high) { channelPriority_ = high ? "high" : "normal"; }
   void set_link_rate(double gbps, const char* kind) {
     linkGBps_ = gbps;
     linkKind_ = kind;
@@ -174,6 +176,7 @@ public:
 private:
   double linkGBps_ = 0;  // measured peer copy rate (ranks of one node), 0 if none
   const char* linkKind_ = "xgmi";  // "xgmi" (distinct GPUs) or "same-device"
+  const char* channelPriority_ = nullptr;
 };
 
 }  // namespace spfft

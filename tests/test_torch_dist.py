@@ -262,6 +262,8 @@ def test_ipc_peer_self_test(gpu):
     code, out = _launch_tool(3, "rccl_probe.py", "UNBUFFERED", "--iters=2", timeout=180)
     assert code == 0, out[-4000:]
     assert out.count("[ipc] self-test: ok") == 3, out[-4000:]
+    # ranks sharing the GPU: normal-priority channel streams (profiles/r6/probe_state)
+    assert out.count("channel priority: normal") == 3, out[-4000:]
 
 
 @pytest.mark.gpu

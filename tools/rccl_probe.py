@@ -70,6 +70,8 @@ def main():
     kind = "" if host else f" [{s.grid.data_plane}]"
     if not host and s.grid.data_plane in ("ipc", "relay"):
         kind += f" self-test: {s.grid.data_plane_info.get('self_test')}"
+    if not host:
+        kind += f" channel priority: {s.grid.data_plane_info.get('channel_priority')}"
     print(f"rank {rank}/{P} {exch_name}{kind} x{iters}: backward err {e1:.2e} forward err {e2:.2e} "
           f"{'OK' if ok else 'FAIL'}", flush=True)
     del s
