@@ -63,7 +63,8 @@ SPFFT_EXPORT SpfftError spfft_amd_grid_exchange_type(SpfftGrid grid, SpfftExchan
 SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane(SpfftGrid grid, const char** name);
 SPFFT_EXPORT SpfftError spfft_amd_float_grid_data_plane(SpfftFloatGrid grid, const char** name);
 /* The data plane's setup facts as a JSON object ("kind"; "self_test",
- * "self_test_ms", "devices", "link_GBps_measured" where they apply). The string
+ * "self_test_ms", "devices", "link_GBps_measured", "channel_priority" where they
+ * apply). The string
  * stays valid until the calling thread's next call of this function.
  * Collective on first call. */
 SPFFT_EXPORT SpfftError spfft_amd_grid_data_plane_info(SpfftGrid grid, const char** json);

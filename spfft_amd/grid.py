@@ -159,7 +159,8 @@ class _GridBase:
     def data_plane_info(self) -> dict:
         """The data plane's setup facts: "kind", and where they apply "self_test" /
         "self_test_ms" (route self-test), "devices" (PCI bus ids of every GPU the plane
-        touches, relay GPUs included), "link_GBps_measured". Collective on first use."""
+        touches, relay GPUs included), "link_GBps_measured", "channel_priority" ("high",
+        or "normal" when ranks share a GPU). Collective on first use."""
         import json
         v = ctypes.c_char_p()
         _check(self._prec.amd_fn("grid_data_plane_info")(self._h, ctypes.byref(v)))
